@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node TEPS of multi-source BFS on RMAT-26 (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+             --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W)
+
+Config (BASELINE.json config 3): RMAT scale 26 (n = 2^26, m = 16 n = 2^30 undirected edges,
+Graph500 A/B/C/D = .57/.19/.19/.05, scrambled ids), 1024 random query groups of 16 sources,
+round-robin across the ranks (main.cu:304-307). Every rank generates the identical graph in its
+own HBM (deterministic counter-based generator, no broadcast) — synthetic data, as the reference
+ships no dataset. One step = the reference's "Computation" phase (main.cu:301-400): BFS of every
+local group + F(U) + the global min-reduction (one RCCL all-reduce). TEPS counts, per group, the
+undirected edges of the components its sources reach (Graph500 convention), summed
+over all 1024 groups, divided by the step time. Total work is fixed as N grows: strong scaling.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "TEPS (whole node) on RMAT-26 multi-source BFS at 1/2/4/8 MI355X"
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scale", type=int, default=26)
+    ap.add_argument("--edgefactor", type=int, default=16)
+    ap.add_argument("--groups", type=int, default=1024)
+    ap.add_argument("--group-size", type=int, default=16)
+    ap.add_argument("--algo", default="bitpar")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--qseed", type=int, default=7)
+    ap.add_argument("--verify", type=int, default=0,
+                    help="check this many groups against the dist solver (untimed)")
+    ap.add_argument("--alpha", type=float, default=0.0)
+    ap.add_argument("--beta", type=float, default=0.0)
+    ap.add_argument("--wide-degree", type=int, default=0)
+    ap.add_argument("--max-words", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import msbfs
+    from msbfs.parallel import distributed as D
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    ctx = D.init_from_env(use_gpu=True)
+    dev = ctx.device
+    t_setup = time.perf_counter()
+    g = msbfs.DeviceGraph.rmat(args.scale, args.edgefactor, args.seed, device=dev)
+    qs = msbfs.QuerySet.random(g.n, args.groups, args.group_size, args.qseed)
+    local_idx = D.round_robin(qs.K, ctx.rank, ctx.world)
+    local_q = qs.subset(local_idx)
+    solver = msbfs.Solver(g, args.algo, max_groups=max(1, local_q.K), alpha=args.alpha,
+                          beta=args.beta, wide_degree=args.wide_degree, max_words=args.max_words)
+    torch.cuda.synchronize(dev)
+    setup_s = time.perf_counter() - t_setup
+
+    # untimed: TEPS numerator (traversed edges per group) — also the first warm-up pass
+    r0 = solver.run(local_q, count_edges=True)
+    total_edges = int(D.allreduce_sum_i64(np.array([int(r0.edges.sum())], np.int64), ctx)[0])
+    if args.verify and ctx.rank == 0:
+        nv = min(args.verify, local_q.K)
+        with msbfs.Solver(g, "dist") as ds:
+            rv = ds.run(local_q.subset(range(nv)))
+        if not np.array_equal(rv.F, r0.F[:nv]):
+            print(f"VERIFY FAILED: bitpar {r0.F[:nv]} vs dist {rv.F}", file=sys.stderr)
+            return 3
+    for _ in range(max(0, args.warmup)):
+        r = solver.run(local_q)
+        D.packed_argmin(r.F, local_idx, qs.K, ctx)
+
+    D.barrier(ctx)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    stats = {}
+    for _ in range(args.steps):
+        r = solver.run(local_q)
+        min_k, min_f = D.packed_argmin(r.F, local_idx, qs.K, ctx)
+        stats = r.stats
+    torch.cuda.synchronize(dev)
+    D.barrier(ctx)
+    dt = time.perf_counter() - t0
+    dt = D.allreduce_max(dt, ctx)  # slowest rank
+    ms = dt / max(1, args.steps) * 1e3
+    value = total_edges / (ms / 1e3) if ms > 0 else 0.0
+    if ctx.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "TEPS",
+            "n_gpus": ctx.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "exact-int (int32 CSR, u64 bitsets)",
+            "data": "synthetic (device-generated Graph500 RMAT, random query groups)",
+            "config": {
+                "model": f"rmat{args.scale}-ef{args.edgefactor}",
+                "global_batch": qs.K,
+                "seq_len": args.group_size,
+                "parallelism": f"dp{ctx.world}",
+                "algo": args.algo,
+                "n": g.n, "m": g.m,
+                "traversed_edges": total_edges,
+                "min_k": int(min_k) + 1, "min_f": int(min_f),
+                "levels": stats.get("levels"), "td_levels": stats.get("td_levels"),
+                "bu_levels": stats.get("bu_levels"), "batches": stats.get("batches"),
+                "setup_s": round(setup_s, 3),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    solver.close()
+    g.close()
+    D.shutdown(ctx)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

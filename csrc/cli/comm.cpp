@@ -1,0 +1,225 @@
+#include "comm.hpp"
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+
+#include "msbfs/device.hpp"
+
+#ifdef MSBFS_HAVE_MPI
+#include <mpi.h>
+#endif
+#ifdef MSBFS_HAVE_RCCL
+#include <rccl/rccl.h>
+#endif
+
+namespace msbfs {
+
+void Comm::bcast_device(void* dptr, size_t bytes, int root, hipStream_t s) {
+  if (size() == 1 || bytes == 0) return;
+  std::vector<char> h(bytes);
+  if (rank() == root) {
+    MSBFS_HIP_CHECK(hipMemcpyAsync(h.data(), dptr, bytes, hipMemcpyDeviceToHost, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  bcast_host(h.data(), bytes, root);
+  if (rank() != root) {
+    MSBFS_HIP_CHECK(hipMemcpyAsync(dptr, h.data(), bytes, hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+}
+
+namespace {
+
+class LocalComm final : public Comm {
+ public:
+  int rank() const override { return 0; }
+  int size() const override { return 1; }
+  std::string name() const override { return "local"; }
+  void barrier() override {}
+  void bcast_host(void*, size_t, int) override {}
+  uint64_t allreduce_min_u64(uint64_t x) override { return x; }
+  void allreduce_sum_i64(int64_t*, size_t) override {}
+  double allreduce_max_f64(double x) override { return x; }
+  void allgather_u64(uint64_t x, std::vector<uint64_t>& out) override { out.assign(1, x); }
+  [[noreturn]] void abort(int code) override { std::exit(code); }
+};
+
+#ifdef MSBFS_HAVE_MPI
+constexpr size_t kChunk = size_t(1) << 30;
+
+class MpiComm : public Comm {
+ public:
+  MpiComm() {
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank_);
+    MPI_Comm_size(MPI_COMM_WORLD, &size_);
+  }
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  std::string name() const override { return "mpi"; }
+  void barrier() override { MPI_Barrier(MPI_COMM_WORLD); }
+  void bcast_host(void* p, size_t bytes, int root) override {
+    char* c = (char*)p;
+    for (size_t off = 0; off < bytes; off += kChunk) {
+      const int cnt = (int)std::min(kChunk, bytes - off);
+      MPI_Bcast(c + off, cnt, MPI_BYTE, root, MPI_COMM_WORLD);
+    }
+  }
+  uint64_t allreduce_min_u64(uint64_t x) override {
+    uint64_t r = x;
+    MPI_Allreduce(&x, &r, 1, MPI_UINT64_T, MPI_MIN, MPI_COMM_WORLD);
+    return r;
+  }
+  void allreduce_sum_i64(int64_t* p, size_t n) override {
+    for (size_t off = 0; off < n; off += kChunk / 8) {
+      const int cnt = (int)std::min(kChunk / 8, n - off);
+      MPI_Allreduce(MPI_IN_PLACE, p + off, cnt, MPI_INT64_T, MPI_SUM, MPI_COMM_WORLD);
+    }
+  }
+  double allreduce_max_f64(double x) override {
+    double r = x;
+    MPI_Allreduce(&x, &r, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    return r;
+  }
+  void allgather_u64(uint64_t x, std::vector<uint64_t>& out) override {
+    out.resize(size_);
+    MPI_Allgather(&x, 1, MPI_UINT64_T, out.data(), 1, MPI_UINT64_T, MPI_COMM_WORLD);
+  }
+  [[noreturn]] void abort(int code) override {
+    // unlike main.cu:98,140 (exit without MPI_Abort -> peers hang in MPI_Bcast), take the job down
+    MPI_Abort(MPI_COMM_WORLD, code);
+    std::exit(code);
+  }
+
+ private:
+  int rank_ = 0, size_ = 1;
+};
+#endif
+
+#if defined(MSBFS_HAVE_MPI) && defined(MSBFS_HAVE_RCCL)
+#define NCCL_CHECK(x)                                                                     \
+  do {                                                                                    \
+    ncclResult_t r_ = (x);                                                                \
+    if (r_ != ncclSuccess) ::msbfs::fail(std::string("RCCL error: ") + ncclGetErrorString(r_)); \
+  } while (0)
+
+class RcclComm final : public Comm {
+ public:
+  RcclComm(std::unique_ptr<Comm> host, int device) : host_(std::move(host)), device_(device) {
+    ncclUniqueId id;
+    if (host_->rank() == 0) NCCL_CHECK(ncclGetUniqueId(&id));
+    host_->bcast_host(&id, sizeof(id), 0);
+    MSBFS_HIP_CHECK(hipSetDevice(device_));
+    MSBFS_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    NCCL_CHECK(ncclCommInitRank(&comm_, host_->size(), id, host_->rank()));
+    MSBFS_HIP_CHECK(hipMalloc(&scratch_, 64));
+  }
+  ~RcclComm() override {
+    if (comm_) ncclCommDestroy(comm_);
+    if (scratch_) (void)hipFree(scratch_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+  int rank() const override { return host_->rank(); }
+  int size() const override { return host_->size(); }
+  std::string name() const override { return "rccl"; }
+  bool device_collectives() const override { return true; }
+  void barrier() override { host_->barrier(); }
+  void bcast_host(void* p, size_t bytes, int root) override { host_->bcast_host(p, bytes, root); }
+  void bcast_device(void* dptr, size_t bytes, int root, hipStream_t s) override {
+    // chunked ring broadcast HBM -> HBM over xGMI
+    const size_t chunk = size_t(1) << 30;
+    for (size_t off = 0; off < bytes; off += chunk)
+      NCCL_CHECK(ncclBroadcast((char*)dptr + off, (char*)dptr + off, std::min(chunk, bytes - off),
+                               ncclInt8, root, comm_, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  uint64_t allreduce_min_u64(uint64_t x) override {
+    MSBFS_HIP_CHECK(hipMemcpyAsync(scratch_, &x, 8, hipMemcpyHostToDevice, stream_));
+    NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclUint64, ncclMin, comm_, stream_));
+    uint64_t r;
+    MSBFS_HIP_CHECK(hipMemcpyAsync(&r, scratch_, 8, hipMemcpyDeviceToHost, stream_));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(stream_));
+    return r;
+  }
+  void allreduce_sum_i64(int64_t* p, size_t n) override {
+    if (!n) return;
+    void* d = nullptr;
+    MSBFS_HIP_CHECK(hipMalloc(&d, n * 8));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(d, p, n * 8, hipMemcpyHostToDevice, stream_));
+    NCCL_CHECK(ncclAllReduce(d, d, n, ncclInt64, ncclSum, comm_, stream_));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(p, d, n * 8, hipMemcpyDeviceToHost, stream_));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(stream_));
+    (void)hipFree(d);
+  }
+  double allreduce_max_f64(double x) override { return host_->allreduce_max_f64(x); }
+  void allgather_u64(uint64_t x, std::vector<uint64_t>& out) override {
+    host_->allgather_u64(x, out);
+  }
+  [[noreturn]] void abort(int code) override {
+    if (comm_) ncclCommAbort(comm_);
+    comm_ = nullptr;
+    host_->abort(code);
+  }
+
+ private:
+  std::unique_ptr<Comm> host_;
+  int device_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  void* scratch_ = nullptr;
+};
+#endif
+
+bool g_mpi_inited = false;
+
+}  // namespace
+
+std::unique_ptr<Comm> make_world_comm(int* argc, char*** argv) {
+#ifdef MSBFS_HAVE_MPI
+  if (!getenv("MSBFS_NO_MPI")) {
+    MPI_Init(argc, argv);
+    g_mpi_inited = true;
+    return std::make_unique<MpiComm>();
+  }
+#endif
+  (void)argc;
+  (void)argv;
+  return std::make_unique<LocalComm>();
+}
+
+std::unique_ptr<Comm> maybe_upgrade_rccl(std::unique_ptr<Comm> host, const std::string& want,
+                                         int device) {
+  if (want == "mpi" || want == "local" || host->size() == 1 || device < 0) return host;
+#if defined(MSBFS_HAVE_MPI) && defined(MSBFS_HAVE_RCCL)
+  // RCCL needs one rank per GPU: check (host, device) pairs are unique across the job.
+  char hn[256] = {0};
+  gethostname(hn, sizeof(hn) - 1);
+  const uint64_t key = (std::hash<std::string>{}(hn) & ~0xFFFFull) | (uint64_t)(device & 0xFFFF);
+  std::vector<uint64_t> keys;
+  host->allgather_u64(key, keys);
+  std::sort(keys.begin(), keys.end());
+  const bool unique = std::adjacent_find(keys.begin(), keys.end()) == keys.end();
+  if (!unique) {
+    if (want == "rccl" && host->rank() == 0)
+      fprintf(stderr, "msbfs: --comm rccl needs one rank per GPU; falling back to MPI\n");
+    return host;
+  }
+  return std::make_unique<RcclComm>(std::move(host), device);
+#else
+  if (want == "rccl" && host->rank() == 0)
+    fprintf(stderr, "msbfs: built without RCCL/MPI; using %s\n", host->name().c_str());
+  return host;
+#endif
+}
+
+void finalize_world() {
+#ifdef MSBFS_HAVE_MPI
+  if (g_mpi_inited) MPI_Finalize();
+#endif
+}
+
+}  // namespace msbfs

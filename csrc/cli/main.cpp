@@ -1,0 +1,345 @@
+// msbfs CLI — drop-in for the reference binary:
+//     mpirun -np <ranks> msbfs -g <graph.bin> -q <query.bin> -gn <numGPU>
+// prints the identical 7-line report (main.cu:403-414). Control flow mirrors main() in
+// main.cu:195-421: bootstrap (:197-201), usage (:204-212), flags (:214-224), device = rank % -gn
+// (:227-228), rank-0 load + broadcast (:237-280), device setup (:282-295), round-robin queries
+// (:303-322), result reduction + argmin (:324-397), report (:402-414).
+//
+// Opt-in extensions (unknown tokens are ignored, like the reference):
+//   --algo {auto,bitpar,dist,topdown,sweep,cpu}   --comm {auto,mpi,rccl,local}
+//   --gen rmat:SCALE:EF:SEED | uniform:N:M:SEED   (per-rank device generation, no broadcast)
+//   --qgen K:SIZE:SEED                            (generated query groups)
+//   --threads N (cpu algo)  --no-cache  --json  --sort-rows  --repeat R
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iomanip>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "comm.hpp"
+#include "msbfs/device.hpp"
+#include "msbfs/graph.hpp"
+
+using namespace msbfs;
+using clk = std::chrono::high_resolution_clock;
+
+namespace {
+
+struct Args {
+  std::string graph, query, algo = "auto", comm = "auto", gen, qgen;
+  int numGPU = 1;
+  int threads = 0;
+  int repeat = 1;
+  bool cache = true, json = false, sort_rows = false;
+};
+
+std::vector<std::string> split(const std::string& s, char d) {
+  std::vector<std::string> out;
+  std::stringstream ss(s);
+  std::string t;
+  while (std::getline(ss, t, d)) out.push_back(t);
+  return out;
+}
+
+int algo_id(const std::string& a) {
+  if (a == "auto") return 0;
+  if (a == "bitpar") return 1;
+  if (a == "dist") return 2;
+  if (a == "topdown") return 3;
+  if (a == "sweep") return 4;
+  if (a == "cpu") return 5;
+  fail("unknown --algo " + a);
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+  auto world = make_world_comm(&argc, &argv);
+  const int world_rank = world->rank();
+
+  if (argc < 5) {  // main.cu:204-212
+    if (world_rank == 0)
+      std::cerr << "Usage: mpirun -np <ranks> " << argv[0]
+                << " -g <graph.bin> -q <query.bin> -gn <numGPU>" << std::endl;
+    finalize_world();
+    return -1;
+  }
+
+  Args a;
+  for (int i = 1; i < argc; i++) {  // exact strcmp flags, unknown tokens ignored (main.cu:216-224)
+    const bool has = i + 1 < argc;
+    if (!strcmp(argv[i], "-g") && has) a.graph = argv[++i];
+    else if (!strcmp(argv[i], "-q") && has) a.query = argv[++i];
+    else if (!strcmp(argv[i], "-gn") && has) a.numGPU = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--algo") && has) a.algo = argv[++i];
+    else if (!strcmp(argv[i], "--comm") && has) a.comm = argv[++i];
+    else if (!strcmp(argv[i], "--gen") && has) a.gen = argv[++i];
+    else if (!strcmp(argv[i], "--qgen") && has) a.qgen = argv[++i];
+    else if (!strcmp(argv[i], "--threads") && has) a.threads = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--repeat") && has) a.repeat = std::max(1, atoi(argv[++i]));
+    else if (!strcmp(argv[i], "--no-cache")) a.cache = false;
+    else if (!strcmp(argv[i], "--json")) a.json = true;
+    else if (!strcmp(argv[i], "--sort-rows")) a.sort_rows = true;
+  }
+
+  try {
+    if (a.numGPU <= 0) fail("-gn must be >= 1 (the reference divides by it, main.cu:227)");
+    const int algo = algo_id(a.algo);
+    const bool cpu = algo == 5;
+
+    int device = -1;
+    if (!cpu) {  // device = world_rank % numGPU (main.cu:227-228), checked
+      int ndev = 0;
+      if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) fail("no GPU visible (use --algo cpu)");
+      device = world_rank % a.numGPU;
+      if (device >= ndev) {
+        if (world_rank == 0)
+          fprintf(stderr, "msbfs: -gn %d exceeds the %d visible GPU(s); using device %d\n",
+                  a.numGPU, ndev, device % ndev);
+        device %= ndev;
+      }
+      MSBFS_HIP_CHECK(hipSetDevice(device));
+    }
+    auto comm = cpu ? std::move(world) : maybe_upgrade_rccl(std::move(world), a.comm, device);
+
+    const auto t_pre0 = clk::now();  // main.cu:235
+
+    // ---- graph: rank-0 load + broadcast, or per-rank deterministic generation -----------------
+    HostCsr hg;
+    DeviceGraph dg;
+    dg.device = std::max(device, 0);
+    hipStream_t stream = nullptr;
+    const bool gen = !a.gen.empty();
+    if (gen) {
+      auto f = split(a.gen, ':');
+      if (f.size() < 2) fail("--gen expects rmat:SCALE:EF:SEED or uniform:N:M:SEED");
+      if (f[0] == "rmat") {
+        const int scale = std::stoi(f[1]);
+        const int64_t ef = f.size() > 2 ? std::stoll(f[2]) : 16;
+        const uint64_t seed = f.size() > 3 ? std::stoull(f[3]) : 1;
+        if (cpu) hg = build_csr(gen_rmat(scale, ef, seed), a.threads);
+        else device_graph_gen_rmat(dg, scale, ef, seed, 0.57, 0.19, 0.19, 1, stream);
+      } else if (f[0] == "uniform") {
+        const int64_t n = std::stoll(f[1]);
+        const int64_t m = f.size() > 2 ? std::stoll(f[2]) : 10 * n;
+        const uint64_t seed = f.size() > 3 ? std::stoull(f[3]) : 1;
+        if (cpu) hg = build_csr(gen_uniform(n, m, seed), a.threads);
+        else device_graph_gen_uniform(dg, n, m, seed, stream);
+      } else {
+        fail("unknown generator " + f[0]);
+      }
+      if (!a.graph.size()) a.graph = a.gen;
+    } else {
+      int64_t hdr[2] = {0, 0};
+      if (comm->rank() == 0) {
+        try {
+          hg = load_graph(a.graph, a.cache, a.threads);
+        } catch (const Error& e) {
+          fprintf(stderr, "%s\n", e.what());  // "Could not open graph file %s" (main.cu:97)
+          comm->abort(EXIT_FAILURE);
+        }
+        hdr[0] = hg.n;
+        hdr[1] = hg.m;
+      }
+      comm->bcast_host(hdr, sizeof(hdr), 0);
+      const int64_t n = hdr[0], m = hdr[1];
+      if (cpu) {
+        if (comm->rank() != 0) {
+          hg.n = n;
+          hg.m = m;
+          hg.rowptr.resize(n + 1);
+          hg.col.resize(2 * m);
+        }
+        comm->bcast_host(hg.rowptr.data(), (n + 1) * sizeof(int64_t), 0);
+        comm->bcast_host(hg.col.data(), 2 * m * sizeof(int32_t), 0);
+      } else if (comm->device_collectives()) {
+        // upload once on rank 0, then HBM -> HBM broadcast over xGMI
+        if (comm->rank() == 0) {
+          device_graph_from_host(dg, n, hg.rowptr.data(), hg.col.data(), stream);
+          hg = HostCsr();
+        } else {
+          dg.n = n;
+          dg.m = m;
+          dg.nnz = 2 * m;
+          dg.own_rowptr.alloc((n + 1) * sizeof(int64_t));
+          dg.own_col.alloc(std::max<int64_t>(1, 2 * m) * sizeof(int32_t));
+          dg.rowptr = dg.own_rowptr.as<int64_t>();
+          dg.col = dg.own_col.as<int32_t>();
+        }
+        MSBFS_HIP_CHECK(hipStreamSynchronize(stream));
+        comm->bcast_device(dg.rowptr, (n + 1) * sizeof(int64_t), 0, stream);
+        comm->bcast_device(dg.col, 2 * m * sizeof(int32_t), 0, stream);
+        if (comm->rank() != 0) device_graph_stats(dg, stream);
+      } else {
+        if (comm->rank() != 0) {
+          hg.n = n;
+          hg.m = m;
+          hg.rowptr.resize(n + 1);
+          hg.col.resize(2 * m);
+        }
+        comm->bcast_host(hg.rowptr.data(), (n + 1) * sizeof(int64_t), 0);
+        comm->bcast_host(hg.col.data(), 2 * m * sizeof(int32_t), 0);
+        device_graph_from_host(dg, n, hg.rowptr.data(), hg.col.data(), stream);
+        hg = HostCsr();
+      }
+    }
+    const int64_t nverts = cpu ? hg.n : dg.n;
+    if (!cpu && a.sort_rows) device_graph_sort_rows(dg, stream);
+
+    // ---- queries: one packed broadcast instead of 2K+1 (main.cu:257-280) ---------------------
+    QuerySet q;
+    if (!a.qgen.empty()) {
+      auto f = split(a.qgen, ':');
+      const int64_t K = std::stoll(f.at(0));
+      const int64_t sz = f.size() > 1 ? std::stoll(f[1]) : 16;
+      const uint64_t seed = f.size() > 2 ? std::stoull(f[2]) : 7;
+      q = gen_queries(nverts, K, sz, seed);
+      if (!a.query.size()) a.query = a.qgen;
+    } else {
+      int64_t qh[2] = {0, 0};
+      if (comm->rank() == 0) {
+        try {
+          q = read_query_bin(a.query);
+        } catch (const Error& e) {
+          fprintf(stderr, "%s\n", e.what());  // "Could not open query file %s" (main.cu:139)
+          comm->abort(EXIT_FAILURE);
+        }
+        qh[0] = q.K();
+        qh[1] = (int64_t)q.ids.size();
+      }
+      comm->bcast_host(qh, sizeof(qh), 0);
+      if (comm->rank() != 0) {
+        q.off.resize(qh[0] + 1);
+        q.ids.resize(qh[1]);
+      }
+      comm->bcast_host(q.off.data(), q.off.size() * sizeof(int64_t), 0);
+      comm->bcast_host(q.ids.data(), q.ids.size() * sizeof(int32_t), 0);
+    }
+    const int64_t K = q.K();
+
+    // ---- static round-robin assignment (main.cu:304-307) -------------------------------------
+    QuerySet local;
+    std::vector<int64_t> local_to_global;
+    for (int64_t k = comm->rank(); k < K; k += comm->size()) {
+      local_to_global.push_back(k);
+      local.ids.insert(local.ids.end(), q.ids.begin() + q.off[k], q.ids.begin() + q.off[k + 1]);
+      local.off.push_back((int64_t)local.ids.size());
+    }
+    const int64_t nlocal = (int64_t)local_to_global.size();
+
+    std::unique_ptr<Solver> solver;
+    if (!cpu) {
+      int dalgo = algo;
+      if (dalgo == 0) dalgo = nlocal > 1 ? 1 : 2;
+      if (dalgo == 1) solver = make_bitpar_solver(dg, (int)std::min<int64_t>(std::max<int64_t>(nlocal, 1), 1024));
+      else if (dalgo == 4) solver = make_sweep_solver(dg);
+      else {
+        solver = make_dist_solver(dg);
+        if (dalgo == 3) solver->opt.force_dir = 1;
+      }
+      if (a.json) solver->opt.count_edges = true;
+      MSBFS_HIP_CHECK(hipDeviceSynchronize());
+    }
+
+    const auto t_pre1 = clk::now();  // main.cu:297-298
+    const double preprocessing_time = std::chrono::duration<double>(t_pre1 - t_pre0).count();
+
+    // ---- computation (main.cu:301-400) ---------------------------------------------------------
+    std::vector<int64_t> F(nlocal, 0), E2(nlocal, 0);
+    double computation_time = 0;
+    int64_t minF = -1, minK = -1;
+    RunStats rs;
+    for (int rep = 0; rep < a.repeat; ++rep) {
+      comm->barrier();
+      const auto t_c0 = clk::now();
+      if (cpu) {
+        HostCsr& g = hg;
+        std::vector<int64_t> e;
+        cpu_msbfs_all(g, local, F, a.json ? &e : nullptr, a.threads > 0 ? a.threads : default_threads());
+        if (a.json)
+          for (int64_t i = 0; i < nlocal; ++i) E2[i] = 2 * e[i];
+      } else if (nlocal) {
+        rs = RunStats();
+        solver->run(nlocal, local.off.data(), local.ids.data(), F.data(), a.json ? E2.data() : nullptr,
+                    &rs, stream);
+      }
+      // packed (F << qbits | q) min-reduce keeps the lowest-index tie-break (main.cu:391-396)
+      int qbits = 1;
+      while ((int64_t(1) << qbits) <= K) ++qbits;
+      int64_t maxF = 0;
+      for (int64_t f : F) maxF = std::max(maxF, f);
+      maxF = (int64_t)comm->allreduce_max_f64((double)maxF);
+      const uint64_t NONE = ~0ull;
+      if (qbits < 63 && (maxF >> (63 - qbits)) == 0) {
+        uint64_t key = NONE;
+        for (int64_t i = 0; i < nlocal; ++i)
+          key = std::min(key, ((uint64_t)F[i] << qbits) | (uint64_t)local_to_global[i]);
+        key = comm->allreduce_min_u64(key);
+        if (key == NONE) { minF = -1; minK = -1; }
+        else { minF = (int64_t)(key >> qbits); minK = (int64_t)(key & ((1ull << qbits) - 1)); }
+      } else {
+        // two-pass fallback when F would not fit next to the query index
+        uint64_t mf = NONE;
+        for (int64_t f : F) mf = std::min(mf, (uint64_t)f);
+        mf = comm->allreduce_min_u64(mf);
+        uint64_t mk = NONE;
+        for (int64_t i = 0; i < nlocal; ++i)
+          if ((uint64_t)F[i] == mf) mk = std::min(mk, (uint64_t)local_to_global[i]);
+        mk = comm->allreduce_min_u64(mk);
+        if (mf == NONE) { minF = -1; minK = -1; }
+        else { minF = (int64_t)mf; minK = (int64_t)mk; }
+      }
+      const auto t_c1 = clk::now();
+      computation_time = std::chrono::duration<double>(t_c1 - t_c0).count();
+    }
+
+    if (comm->rank() == 0) {  // main.cu:403-414
+      std::cout << std::fixed << std::setprecision(9);
+      std::cout << "Graph: " << a.graph << "\n";
+      std::cout << "Query: " << a.query << "\n";
+      std::cout << "Query number (k) with minimum F value: " << (minK + 1) << "\n";
+      std::cout << "Minimum F value: " << minF << "\n";
+      std::cout << "GPU # : " << a.numGPU << " GPU\n";
+      std::cout << "Preprocessing time: " << preprocessing_time << " s\n";
+      std::cout << "Computation time: " << computation_time << " s\n";
+      std::cout.flush();
+    }
+    if (a.json) {
+      // full F vector + TEPS accounting (Graph500: traversed edges = reached degree sum / 2)
+      std::vector<int64_t> allF(K, 0), allE(K, 0);
+      for (int64_t i = 0; i < nlocal; ++i) {
+        allF[local_to_global[i]] = F[i];
+        allE[local_to_global[i]] = E2[i];
+      }
+      comm->allreduce_sum_i64(allF.data(), K);
+      comm->allreduce_sum_i64(allE.data(), K);
+      const double tmax = comm->allreduce_max_f64(computation_time);
+      if (comm->rank() == 0) {
+        double edges = 0;
+        for (int64_t e : allE) edges += 0.5 * (double)e;
+        std::cout << "{\"K\": " << K << ", \"n\": " << nverts << ", \"ranks\": " << comm->size()
+                  << ", \"comm\": \"" << comm->name() << "\", \"algo\": \"" << a.algo
+                  << "\", \"traversed_edges\": " << std::setprecision(0) << edges
+                  << ", \"teps\": " << std::setprecision(3) << (tmax > 0 ? edges / tmax : 0)
+                  << ", \"levels\": " << rs.levels << ", \"td_levels\": " << rs.td_levels
+                  << ", \"bu_levels\": " << rs.bu_levels << ", \"F\": [";
+        for (int64_t k = 0; k < K; ++k) std::cout << (k ? ", " : "") << allF[k];
+        std::cout << "]}" << std::endl;
+      }
+    }
+    solver.reset();
+    comm.reset();
+  } catch (const std::exception& e) {
+    fprintf(stderr, "msbfs: %s\n", e.what());
+    finalize_world();
+    return EXIT_FAILURE;
+  }
+  finalize_world();
+  return 0;
+}

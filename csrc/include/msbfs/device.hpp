@@ -1,0 +1,163 @@
+// Internal device-side infrastructure shared by the HIP translation units: error checks,
+// device buffers, the device CSR, wave64 helpers and the solver interfaces.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "msbfs/common.hpp"
+
+#define MSBFS_HIP_CHECK(expr)                                                                \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      ::msbfs::fail(std::string("HIP error '") + hipGetErrorString(_e) + "' at " __FILE__ ":" + \
+                    std::to_string(__LINE__) + " in " #expr);                                \
+  } while (0)
+
+namespace msbfs {
+
+// Owning device allocation (RAII). Graph-sized buffers are allocated once and reused for every
+// query group / batch: the reference cudaMalloc/cudaFree's a flag per query (main.cu:57,72).
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  explicit DevBuf(size_t b) { alloc(b); }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    release();
+    p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0;
+    return *this;
+  }
+  ~DevBuf() { release(); }
+  void alloc(size_t b) {
+    release();
+    if (b == 0) b = 16;
+    MSBFS_HIP_CHECK(hipMalloc(&p, b));
+    bytes = b;
+  }
+  void ensure(size_t b) { if (b > bytes) alloc(b); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T> T* as() const { return (T*)p; }
+};
+
+// Pinned host staging buffer (for per-level counter read-back without pageable copies; the
+// reference does 1-byte synchronous pageable copies every level, main.cu:64,69).
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  explicit PinnedBuf(size_t b) : bytes(b) { MSBFS_HIP_CHECK(hipHostMalloc(&p, b, hipHostMallocDefault)); }
+  ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+  PinnedBuf(const PinnedBuf&) = delete;
+  PinnedBuf& operator=(const PinnedBuf&) = delete;
+  template <class T> T* as() const { return (T*)p; }
+};
+
+// Device-resident symmetric CSR (int64 offsets, int32 columns). Either owns its arrays or
+// borrows externally-owned ones (e.g. torch tensors handed over from Python).
+struct DeviceGraph {
+  int device = 0;
+  int64_t n = 0, nnz = 0, m = 0;
+  int64_t* rowptr = nullptr;
+  int32_t* col = nullptr;
+  DevBuf own_rowptr, own_col;
+  int64_t max_degree = 0;
+  int64_t isolated = 0;
+};
+
+// Stats returned by solvers (mirrors msbfs_stats in msbfs.h).
+struct RunStats {
+  int64_t levels = 0, td_levels = 0, bu_levels = 0, batches = 0;
+  double device_ms = 0;
+};
+
+// ---- device-graph construction (kernels/gen.hip) -------------------------------------------
+void device_graph_from_host(DeviceGraph& g, int64_t n, const int64_t* rowptr, const int32_t* col,
+                            hipStream_t s);
+void device_graph_from_edges(DeviceGraph& g, int64_t n, int64_t m, const int32_t* d_u,
+                             const int32_t* d_v, hipStream_t s);
+void device_graph_gen_rmat(DeviceGraph& g, int scale, int64_t edgefactor, uint64_t seed, double a,
+                           double b, double c, int scramble, hipStream_t s);
+void device_graph_gen_uniform(DeviceGraph& g, int64_t n, int64_t m, uint64_t seed, hipStream_t s);
+void device_graph_stats(DeviceGraph& g, hipStream_t s);
+void device_graph_sort_rows(DeviceGraph& g, hipStream_t s);
+
+// ---- solvers ---------------------------------------------------------------------------------
+struct SolverOptions {
+  double alpha = 14.0;  // top-down -> bottom-up when frontier edges > unexplored edges / alpha
+  double beta = 24.0;   // bottom-up -> top-down when frontier vertices < active vertices / beta
+  int wide_degree = 64; // bottom-up: vertices above this degree get a whole wave
+  int force_dir = 0;    // 0 auto, 1 top-down only, 2 bottom-up after level 0
+  int max_words = 16;   // bit-parallel: at most 64*max_words groups per batch
+  bool count_edges = false;
+};
+
+class Solver {
+ public:
+  virtual ~Solver() = default;
+  // Runs groups [0,K) of a packed query set; F[k] and (optionally) edges2[k] (= sum of degrees
+  // of reached vertices, i.e. 2x the Graph500 traversed-edge count) are written to host memory.
+  virtual void run(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t* F,
+                   int64_t* edges2, RunStats* st, hipStream_t stream) = 0;
+  SolverOptions opt;
+};
+
+std::unique_ptr<Solver> make_bitpar_solver(const DeviceGraph& g, int max_groups);
+std::unique_ptr<Solver> make_dist_solver(const DeviceGraph& g);
+std::unique_ptr<Solver> make_sweep_solver(const DeviceGraph& g);
+
+// ---- common level-loop helpers (kernels/lbs.hip) ---------------------------------------------
+// Inclusive prefix sum of the degrees of `list[0..cnt)` into offs[0..cnt) (int64).
+size_t frontier_scan_temp_bytes(int64_t max_items);
+void frontier_degree_scan(const int64_t* rowptr, const int32_t* list, int64_t cnt, int64_t* offs,
+                          void* temp, size_t temp_bytes, hipStream_t s);
+
+inline int grid_for(int64_t items, int per_block, int cap = 2048) {
+  int64_t g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace msbfs
+
+#if defined(__HIPCC__)
+// ---- wave64 device helpers ---------------------------------------------------------------
+namespace msbfs {
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int l = lane_id();
+  return l ? (~0ull >> (64 - l)) : 0ull;
+}
+// Wave-aggregated append: every lane with pred gets a unique slot of *counter. Must be called
+// by all lanes that are active in the enclosing control flow.
+__device__ __forceinline__ uint32_t wave_append(bool pred, uint32_t* counter) {
+  const uint64_t mask = __ballot(pred);
+  if (!mask) return 0;
+  const int leader = __ffsll((unsigned long long)mask) - 1;
+  uint32_t base = 0;
+  if (lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+  base = __shfl(base, leader);
+  return base + (uint32_t)__popcll(mask & lanemask_lt());
+}
+__device__ __forceinline__ int64_t upper_bound_i64(const int64_t* a, int64_t cnt, int64_t x) {
+  int64_t lo = 0, hi = cnt;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+}  // namespace msbfs
+#endif

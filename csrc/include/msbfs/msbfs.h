@@ -1,0 +1,105 @@
+/* msbfs — MI355X-native multi-source BFS / distance-to-set engine. Public C API.
+ *
+ * Capability parity with the reference (irmakerkol/Parallel-Multi-Source-BFS-Implementation-
+ * Using-MPI-and-CUDA, main.cu): binary edge-list graph + query loaders (main.cu:92-164),
+ * symmetric CSR, per-group multi-source BFS + F(U) (main.cu:16-89), round-robin distribution
+ * and global argmin (main.cu:303-397). All functions return 0 on success and a negative value
+ * on error; msbfs_last_error() returns the thread-local message.
+ */
+#ifndef MSBFS_H_
+#define MSBFS_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct msbfs_graph_s* msbfs_graph;
+typedef struct msbfs_solver_s* msbfs_solver;
+
+enum msbfs_algo {
+  MSBFS_ALGO_AUTO = 0,    /* bit-parallel when K > 1, else dist */
+  MSBFS_ALGO_BITPAR = 1,  /* 64*W groups per pass, direction optimising */
+  MSBFS_ALGO_DIST = 2,    /* one distance array per group, direction optimising */
+  MSBFS_ALGO_TOPDOWN = 3, /* dist path, top-down only (queue + load-balanced edges) */
+  MSBFS_ALGO_SWEEP = 4,   /* reference algorithm: thread per vertex, full sweep per level */
+  MSBFS_ALGO_CPU = 5      /* host threads (oracle / "serial CPU BFS" config) */
+};
+
+typedef struct {
+  int64_t levels, td_levels, bu_levels, batches;
+  double device_ms;
+} msbfs_stats;
+
+typedef struct {
+  double alpha, beta;
+  int wide_degree, force_dir, max_words;
+} msbfs_options;
+
+const char* msbfs_last_error(void);
+const char* msbfs_version(void);
+void msbfs_free(void* p);
+
+/* ---- devices ---- */
+int msbfs_device_count(int* n);
+int msbfs_set_device(int dev);
+int msbfs_device_sync(void);
+
+/* ---- host formats / generators (buffers returned via malloc; free with msbfs_free) ---- */
+int msbfs_read_graph_csr(const char* path, int use_cache, int64_t* n, int64_t* m,
+                         int64_t** rowptr, int32_t** col);
+int msbfs_read_edge_list(const char* path, int64_t* n, int64_t* m, int32_t** u, int32_t** v);
+int msbfs_write_edge_list(const char* path, int64_t n, int64_t m, const int32_t* u,
+                          const int32_t* v);
+int msbfs_read_queries(const char* path, int64_t* K, int64_t** off, int64_t* nids, int32_t** ids);
+int msbfs_write_queries(const char* path, int64_t K, const int64_t* off, const int32_t* ids,
+                        int force_extended);
+int msbfs_build_csr(int64_t n, int64_t m, const int32_t* u, const int32_t* v, int stable,
+                    int64_t** rowptr, int32_t** col);
+int msbfs_gen_rmat_host(int scale, int64_t edgefactor, uint64_t seed, double a, double b, double c,
+                        int scramble, int32_t** u, int32_t** v, int64_t* n, int64_t* m);
+int msbfs_gen_uniform_host(int64_t n, int64_t m, uint64_t seed, int32_t** u, int32_t** v);
+int msbfs_gen_grid_host(int64_t rows, int64_t cols, double keep, int64_t shortcuts, uint64_t seed,
+                        int32_t** u, int32_t** v, int64_t* n, int64_t* m);
+int msbfs_gen_queries(int64_t n, int64_t K, int64_t size, uint64_t seed, int64_t** off,
+                      int32_t** ids);
+
+/* ---- CPU BFS (query-parallel host threads) ---- */
+int msbfs_cpu_run(int64_t n, const int64_t* rowptr, const int32_t* col, int64_t K,
+                  const int64_t* qoff, const int32_t* qids, int64_t* F, int64_t* edges,
+                  int nthreads);
+
+/* ---- device graphs ---- */
+int msbfs_graph_from_host_csr(int device, int64_t n, const int64_t* rowptr, const int32_t* col,
+                              msbfs_graph* out);
+int msbfs_graph_from_device_edges(int device, int64_t n, int64_t m, const int32_t* d_u,
+                                  const int32_t* d_v, msbfs_graph* out);
+int msbfs_graph_wrap_device(int device, int64_t n, int64_t nnz, int64_t* d_rowptr, int32_t* d_col,
+                            msbfs_graph* out);
+int msbfs_graph_gen_rmat(int device, int scale, int64_t edgefactor, uint64_t seed, double a,
+                         double b, double c, int scramble, msbfs_graph* out);
+int msbfs_graph_gen_uniform(int device, int64_t n, int64_t m, uint64_t seed, msbfs_graph* out);
+int msbfs_graph_sort_rows(msbfs_graph g);
+int msbfs_graph_info(msbfs_graph g, int64_t* n, int64_t* nnz, int64_t* m, int64_t* max_degree,
+                     int64_t* isolated);
+int msbfs_graph_device_ptrs(msbfs_graph g, void** rowptr, void** col);
+int msbfs_graph_download(msbfs_graph g, int64_t* rowptr, int32_t* col);
+void msbfs_graph_free(msbfs_graph g);
+
+/* ---- solvers ---- */
+int msbfs_solver_create(msbfs_graph g, int algo, int64_t max_groups, msbfs_solver* out);
+int msbfs_solver_set_options(msbfs_solver s, const msbfs_options* o);
+/* F[k] for k in [0,K); edges2 (nullable) = per-group sum of reached degrees (2x the Graph500
+ * traversed-edge count). stream = hipStream_t or NULL for the null stream. */
+int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32_t* qids,
+                     int64_t* F, int64_t* edges2, msbfs_stats* st, void* stream);
+void msbfs_solver_free(msbfs_solver s);
+
+/* reference argmin (main.cu:381-397): first valid, strict '<', lowest index wins ties; -1 if K=0 */
+int64_t msbfs_argmin(const int64_t* F, int64_t K);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSBFS_H_ */

@@ -1,0 +1,326 @@
+// Binary graph/query I/O, parallel CSR build and the CSR sidecar cache.
+//
+// Reference: LoadGraphBin main.cu:92-130 (per-element fread, vector<vector<int>> adjacency,
+// int32 offsets) and LoadQueryBin main.cu:134-164 (uint8 K, uint8 sizes). Here the file is
+// mmap'd, validated (truncation, id range — UB in the reference), and turned into an
+// int64-offset CSR by a multi-threaded count -> scan -> scatter.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+
+#include "msbfs/graph.hpp"
+
+namespace msbfs {
+
+void fail(const std::string& msg) { throw Error(msg); }
+
+int default_threads() {
+  unsigned hc = std::thread::hardware_concurrency();
+  if (const char* e = getenv("OMP_NUM_THREADS")) {
+    int v = atoi(e);
+    if (v > 0) return v;
+  }
+  return hc ? (int)std::min(hc, 64u) : 4;
+}
+
+template <class F>
+static void parallel_for(int nthreads, int64_t total, F&& fn) {
+  if (nthreads <= 1 || total < 65536) {
+    fn(0, total, 0);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t chunk = (total + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; ++t) {
+    const int64_t b = t * chunk, e = std::min(total, b + chunk);
+    if (b >= e) break;
+    th.emplace_back([&fn, b, e, t] { fn(b, e, t); });
+  }
+  for (auto& x : th) x.join();
+}
+
+namespace {
+struct MappedFile {
+  int fd = -1;
+  void* p = nullptr;
+  size_t size = 0;
+  int64_t mtime = 0;
+  explicit MappedFile(const std::string& path, const char* what) {
+    fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) fail(std::string("Could not open ") + what + " file " + path);
+    struct stat st;
+    if (fstat(fd, &st) != 0) fail("stat failed on " + path);
+    size = (size_t)st.st_size;
+    mtime = (int64_t)st.st_mtime;
+    if (size) {
+      p = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+      if (p == MAP_FAILED) fail("mmap failed on " + path);
+      madvise(p, size, MADV_SEQUENTIAL);
+    }
+  }
+  ~MappedFile() {
+    if (p && p != MAP_FAILED) munmap(p, size);
+    if (fd >= 0) ::close(fd);
+  }
+  const uint8_t* bytes() const { return (const uint8_t*)p; }
+};
+
+void write_all(FILE* f, const void* p, size_t n, const std::string& path) {
+  if (n && fwrite(p, 1, n, f) != n) fail("short write to " + path);
+}
+}  // namespace
+
+EdgeList read_edge_list_bin(const std::string& path) {
+  MappedFile mf(path, "graph");
+  if (mf.size < 12) fail("graph file " + path + " is truncated (need 12-byte header)");
+  int32_t n;
+  int64_t m;
+  std::memcpy(&n, mf.bytes(), 4);
+  std::memcpy(&m, mf.bytes() + 4, 8);
+  if (n < 0 || m < 0) fail("graph file " + path + " has a negative n or m");
+  const uint64_t need = 12ull + 8ull * (uint64_t)m;
+  if (mf.size < need)
+    fail("graph file " + path + " is truncated: header says m=" + std::to_string(m) +
+         " edges but the file holds " + std::to_string((mf.size - 12) / 8));
+  EdgeList el;
+  el.n = n;
+  el.u.resize(m);
+  el.v.resize(m);
+  const uint8_t* base = mf.bytes() + 12;
+  std::atomic<int64_t> bad{-1};
+  parallel_for(default_threads(), m, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) {
+      int32_t uv[2];
+      std::memcpy(uv, base + 8 * i, 8);
+      el.u[i] = uv[0];
+      el.v[i] = uv[1];
+      if ((uint32_t)uv[0] >= (uint32_t)n || (uint32_t)uv[1] >= (uint32_t)n) {
+        int64_t exp = -1;
+        bad.compare_exchange_strong(exp, i);
+      }
+    }
+  });
+  if (bad.load() >= 0)
+    fail("graph file " + path + ": edge " + std::to_string(bad.load()) +
+         " has a vertex id outside [0, n)");
+  return el;
+}
+
+void write_edge_list_bin(const std::string& path, const EdgeList& el) {
+  if (el.n > INT32_MAX) fail("legacy graph format stores n as int32");
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) fail("Could not open graph file " + path + " for writing");
+  const int32_t n = (int32_t)el.n;
+  const int64_t m = el.m();
+  write_all(f, &n, 4, path);
+  write_all(f, &m, 8, path);
+  std::vector<int32_t> buf;
+  const int64_t B = 1 << 20;
+  for (int64_t i = 0; i < m; i += B) {
+    const int64_t e = std::min(m, i + B);
+    buf.resize(2 * (e - i));
+    for (int64_t j = i; j < e; ++j) {
+      buf[2 * (j - i)] = el.u[j];
+      buf[2 * (j - i) + 1] = el.v[j];
+    }
+    write_all(f, buf.data(), buf.size() * 4, path);
+  }
+  if (fclose(f) != 0) fail("close failed on " + path);
+}
+
+static const char kQxMagic[8] = {'M', 'S', 'B', 'F', 'S', 'Q', 'X', '1'};
+
+QuerySet read_query_bin(const std::string& path) {
+  MappedFile mf(path, "query");
+  const uint8_t* p = mf.bytes();
+  const size_t sz = mf.size;
+  QuerySet q;
+  if (sz < 1) fail("query file " + path + " is empty (need at least the K byte)");
+  size_t pos = 0;
+  auto need = [&](size_t k) {
+    if (pos + k > sz) fail("query file " + path + " is truncated at byte " + std::to_string(pos));
+  };
+  if (p[0] == 0 && sz >= 1 + 8 + 4 && std::memcmp(p + 1, kQxMagic, 8) == 0) {
+    // extended format
+    pos = 9;
+    uint32_t K;
+    std::memcpy(&K, p + pos, 4);
+    pos += 4;
+    q.off.reserve(K + 1);
+    for (uint32_t k = 0; k < K; ++k) {
+      need(4);
+      uint32_t s;
+      std::memcpy(&s, p + pos, 4);
+      pos += 4;
+      need(4ull * s);
+      const size_t base = q.ids.size();
+      q.ids.resize(base + s);
+      std::memcpy(q.ids.data() + base, p + pos, 4ull * s);
+      pos += 4ull * s;
+      q.off.push_back((int64_t)q.ids.size());
+    }
+    return q;
+  }
+  // legacy format: uint8 K, then K x {uint8 size, size x int32} (main.cu:143-160)
+  const int K = p[0];
+  pos = 1;
+  for (int k = 0; k < K; ++k) {
+    need(1);
+    const int s = p[pos++];
+    need(4ull * s);
+    const size_t base = q.ids.size();
+    q.ids.resize(base + s);
+    std::memcpy(q.ids.data() + base, p + pos, 4ull * s);
+    pos += 4ull * s;
+    q.off.push_back((int64_t)q.ids.size());
+  }
+  return q;
+}
+
+void write_query_bin(const std::string& path, const QuerySet& q, bool force_extended) {
+  const int64_t K = q.K();
+  bool ext = force_extended || K > 255;
+  for (int64_t k = 0; k < K && !ext; ++k) ext = (q.off[k + 1] - q.off[k]) > 255;
+  if (ext && K == 0) ext = true;
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) fail("Could not open query file " + path + " for writing");
+  if (!ext) {
+    const uint8_t k8 = (uint8_t)K;
+    write_all(f, &k8, 1, path);
+    for (int64_t k = 0; k < K; ++k) {
+      const uint8_t s = (uint8_t)(q.off[k + 1] - q.off[k]);
+      write_all(f, &s, 1, path);
+      write_all(f, q.ids.data() + q.off[k], 4ull * s, path);
+    }
+  } else {
+    if (K > UINT32_MAX) fail("too many query groups");
+    const uint8_t z = 0;
+    const uint32_t k32 = (uint32_t)K;
+    write_all(f, &z, 1, path);
+    write_all(f, kQxMagic, 8, path);
+    write_all(f, &k32, 4, path);
+    for (int64_t k = 0; k < K; ++k) {
+      const uint32_t s = (uint32_t)(q.off[k + 1] - q.off[k]);
+      write_all(f, &s, 4, path);
+      write_all(f, q.ids.data() + q.off[k], 4ull * s, path);
+    }
+  }
+  if (fclose(f) != 0) fail("close failed on " + path);
+}
+
+HostCsr build_csr(const EdgeList& el, int nthreads, bool stable) {
+  if (nthreads <= 0) nthreads = default_threads();
+  HostCsr g;
+  g.n = el.n;
+  g.m = el.m();
+  const int64_t n = el.n, m = el.m();
+  g.rowptr.assign(n + 1, 0);
+  int64_t* deg = g.rowptr.data() + 1;
+  parallel_for(nthreads, m, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) {
+      __atomic_fetch_add(&deg[el.u[i]], 1, __ATOMIC_RELAXED);
+      __atomic_fetch_add(&deg[el.v[i]], 1, __ATOMIC_RELAXED);
+    }
+  });
+  for (int64_t i = 0; i < n; ++i) g.rowptr[i + 1] += g.rowptr[i];
+  g.col.resize(2 * m);
+  std::vector<int64_t> cur(g.rowptr.begin(), g.rowptr.end() - 1);
+  if (stable || nthreads <= 1 || m < 65536) {
+    // exact reference neighbour order: adj[u] += v; adj[v] += u in file order
+    for (int64_t i = 0; i < m; ++i) {
+      g.col[cur[el.u[i]]++] = el.v[i];
+      g.col[cur[el.v[i]]++] = el.u[i];
+    }
+  } else {
+    parallel_for(nthreads, m, [&](int64_t b, int64_t e, int) {
+      for (int64_t i = b; i < e; ++i) {
+        const int32_t u = el.u[i], v = el.v[i];
+        g.col[__atomic_fetch_add(&cur[u], 1, __ATOMIC_RELAXED)] = v;
+        g.col[__atomic_fetch_add(&cur[v], 1, __ATOMIC_RELAXED)] = u;
+      }
+    });
+  }
+  return g;
+}
+
+static const char kCsrMagic[8] = {'M', 'S', 'B', 'F', 'S', 'C', 'R', '1'};
+
+void write_csr_cache(const std::string& path, const HostCsr& g, uint64_t src_size,
+                     int64_t src_mtime) {
+  const std::string tmp = path + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) return;  // cache is best-effort
+  write_all(f, kCsrMagic, 8, tmp);
+  write_all(f, &src_size, 8, tmp);
+  write_all(f, &src_mtime, 8, tmp);
+  write_all(f, &g.n, 8, tmp);
+  write_all(f, &g.m, 8, tmp);
+  write_all(f, g.rowptr.data(), 8 * g.rowptr.size(), tmp);
+  write_all(f, g.col.data(), 4 * g.col.size(), tmp);
+  fclose(f);
+  rename(tmp.c_str(), path.c_str());
+}
+
+bool read_csr_cache(const std::string& path, HostCsr& g, uint64_t src_size, int64_t src_mtime) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  char magic[8];
+  uint64_t sz;
+  int64_t mt, n, m;
+  bool ok = fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kCsrMagic, 8) == 0 &&
+            fread(&sz, 8, 1, f) == 1 && fread(&mt, 8, 1, f) == 1 && fread(&n, 8, 1, f) == 1 &&
+            fread(&m, 8, 1, f) == 1 && sz == src_size && mt == src_mtime && n >= 0 && m >= 0;
+  if (ok) {
+    g.n = n;
+    g.m = m;
+    g.rowptr.resize(n + 1);
+    g.col.resize(2 * m);
+    ok = fread(g.rowptr.data(), 8, n + 1, f) == (size_t)(n + 1) &&
+         fread(g.col.data(), 4, 2 * m, f) == (size_t)(2 * m) && g.rowptr.back() == 2 * m;
+  }
+  fclose(f);
+  return ok;
+}
+
+HostCsr load_graph(const std::string& path, bool use_cache, int nthreads) {
+  uint64_t size = 0;
+  int64_t mtime = 0;
+  {
+    struct stat st;
+    if (stat(path.c_str(), &st) != 0) fail("Could not open graph file " + path);
+    size = (uint64_t)st.st_size;
+    mtime = (int64_t)st.st_mtime;
+  }
+  HostCsr g;
+  const std::string cpath = path + ".csr";
+  if (use_cache && read_csr_cache(cpath, g, size, mtime)) return g;
+  EdgeList el = read_edge_list_bin(path);
+  g = build_csr(el, nthreads, false);
+  if (use_cache) write_csr_cache(cpath, g, size, mtime);
+  return g;
+}
+
+int64_t argmin_first(const std::vector<int64_t>& F) {
+  int64_t minF = -1, minK = -1;
+  for (size_t i = 0; i < F.size(); ++i)
+    if (F[i] >= 0) {
+      minF = F[i];
+      minK = (int64_t)i;
+      break;
+    }
+  for (size_t i = 0; i < F.size(); ++i)
+    if (F[i] < minF && F[i] >= 0) {
+      minF = F[i];
+      minK = (int64_t)i;
+    }
+  return minK;
+}
+
+}  // namespace msbfs

@@ -1,0 +1,789 @@
+// Bit-parallel, direction-optimising multi-source BFS over up to 64*W query groups at once.
+//
+// What it replaces: the reference runs each query group as its own level-synchronous BFS with a
+// thread-per-vertex kernel that rescans all n distances every level (BFSKernal main.cu:16-38,
+// driven by GPUMultiSourceBFS main.cu:40-73), then copies all n distances to the host to sum them
+// (ComputeFofU main.cu:75-89). Queries run strictly one after another per rank
+// (main.cu:312-322).
+//
+// Here one pass over the graph advances 64*W groups together (MS-BFS, Then et al. VLDB'15):
+//  * every vertex owns W 64-bit words: bit k of word j = "visited by group 64j+k".
+//  * top-down levels (small frontiers) push frontier bits along edges with 64-bit atomicOr into
+//    an accumulator, edge-parallel via a load-balanced search over the frontier's degree prefix
+//    (no hub serialisation);
+//  * bottom-up levels (large frontiers) pull: an unfinished vertex ORs its neighbours' visited
+//    words and stops as soon as every still-alive group is covered (early exit). Double-buffered
+//    visited arrays make the pull race-free without a separate frontier array (a neighbour bit
+//    visited at any level <= L can only have been set exactly at L if it is still missing here).
+//  * per-group F(U) = sum_level level * |newly visited| is accumulated on chip: every new bit adds
+//    `level` to a per-group LDS counter; one global atomic per group per block at the end. Only
+//    8 bytes per group ever leave the device (vs 4n bytes per query in the reference).
+//  * groups whose frontier died are masked out ("alive" words), so groups stuck in small
+//    components never stop other groups' vertices from finishing.
+// Lane mapping for wave64: each lane owns VW (1-2) words = one 8-16 B load, a vertex's W words are
+// spread over G = W/VW consecutive lanes, so W=16 reads a vertex's 128-B line in one coalesced
+// wave-instruction slice.
+#include <algorithm>
+#include <cstring>
+
+#include "msbfs/device.hpp"
+
+namespace msbfs {
+namespace bp {
+
+constexpr int kBlock = 256;
+
+template <int W>
+struct Lay {
+  static constexpr int VW = W >= 2 ? 2 : 1;
+  static constexpr int G = W / VW;      // lanes per vertex
+  static constexpr int VPW = 64 / G;    // vertices per wave
+  static constexpr uint64_t GBITS = (G == 64) ? ~0ull : ((1ull << G) - 1);
+};
+
+template <int VW>
+struct V {
+  uint64_t w[VW];
+};
+
+template <int VW>
+__device__ __forceinline__ V<VW> ldv(const uint64_t* p) {
+  V<VW> r;
+  if constexpr (VW == 2) {
+    typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+    const u2 x = *(const u2*)p;
+    r.w[0] = x.x;
+    r.w[1] = x.y;
+  } else {
+    r.w[0] = *p;
+  }
+  return r;
+}
+template <int VW>
+__device__ __forceinline__ void stv(uint64_t* p, const V<VW>& v) {
+  if constexpr (VW == 2) {
+    typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+    u2 x;
+    x.x = v.w[0];
+    x.y = v.w[1];
+    *(u2*)p = x;
+  } else {
+    *p = v.w[0];
+  }
+}
+template <int VW>
+__device__ __forceinline__ V<VW> vzero() {
+  V<VW> r;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) r.w[j] = 0;
+  return r;
+}
+
+struct Ctr {
+  uint32_t act2, actw2, fl2, touched;
+  unsigned long long ef2;  // sum of degrees of the next frontier
+  unsigned long long eu2;  // sum of degrees of the next active lists
+  uint32_t newcnt;          // vertices with new bits (== fl2)
+  uint32_t pad[3];
+};
+
+__device__ __forceinline__ bool is_done(const uint32_t* done, int32_t v) {
+  return (done[v >> 5] >> (v & 31)) & 1u;
+}
+__device__ __forceinline__ void set_done(uint32_t* done, int32_t v) {
+  atomicOr(&done[v >> 5], 1u << (v & 31));
+}
+
+// sum a per-lane value over the wave and add it once to *dst (must be called converged)
+__device__ __forceinline__ void wave_sum_add(unsigned long long val, unsigned long long* dst) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
+  if (lane_id() == 0 && val) atomicAdd(dst, val);
+}
+
+template <int W, bool COUNT>
+struct Lds {
+  uint32_t f[64 * W];
+  unsigned long long e[COUNT ? 64 * W : 1];
+};
+
+template <int W, bool COUNT>
+__device__ __forceinline__ void lds_zero(Lds<W, COUNT>& s) {
+  for (int i = threadIdx.x; i < 64 * W; i += blockDim.x) {
+    s.f[i] = 0;
+    if constexpr (COUNT) s.e[i] = 0;
+  }
+  __syncthreads();
+}
+
+template <int W, bool COUNT>
+__device__ __forceinline__ void count_bits(Lds<W, COUNT>& s, const V<Lay<W>::VW>& nw, int slot,
+                                           uint32_t deg) {
+  constexpr int VW = Lay<W>::VW;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    uint64_t x = nw.w[j];
+    const int base = (slot * VW + j) * 64;
+    while (x) {
+      const int b = __ffsll((unsigned long long)x) - 1;
+      x &= x - 1;
+      atomicAdd(&s.f[base + b], 1u);
+      if constexpr (COUNT) atomicAdd(&s.e[base + b], (unsigned long long)deg);
+    }
+  }
+}
+
+template <int W, bool COUNT>
+__device__ __forceinline__ void lds_flush(Lds<W, COUNT>& s, unsigned long long* F,
+                                          unsigned long long* E, uint64_t* alive_next,
+                                          uint32_t level) {
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * W; i += blockDim.x) {
+    const uint32_t c = s.f[i];
+    if (c) {
+      atomicAdd(&F[i], (unsigned long long)c * level);
+      atomicOr((unsigned long long*)&alive_next[i >> 6], 1ull << (i & 63));
+    }
+    if constexpr (COUNT) {
+      if (s.e[i]) atomicAdd(&E[i], s.e[i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// init: scatter the batch's sources (v, local group) into both visited buffers and the
+// top-down accumulator; dedupe vertices into the first frontier list via stamps.
+// ---------------------------------------------------------------------------------------------
+template <int W, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_t* pk, int64_t np,
+                                                 const int64_t* rowptr, uint64_t* visA,
+                                                 uint64_t* visB, uint64_t* acc, int32_t* stamp,
+                                                 int32_t epoch, int32_t* fl, Ctr* ctr,
+                                                 unsigned long long* E, uint64_t* alive) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t lim = (np + stride - 1) / stride * stride;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
+    bool app = false;
+    int32_t v = 0;
+    unsigned long long deg = 0;
+    if (i < np) {
+      v = pv[i];
+      const int k = pk[i];
+      const int word = k >> 6;
+      const uint64_t bit = 1ull << (k & 63);
+      const uint64_t old = atomicOr((unsigned long long*)&visA[(int64_t)v * W + word], bit);
+      if (!(old & bit)) {
+        atomicOr((unsigned long long*)&visB[(int64_t)v * W + word], bit);
+        atomicOr((unsigned long long*)&acc[(int64_t)v * W + word], bit);
+        atomicOr((unsigned long long*)&alive[word], bit);
+        deg = (unsigned long long)(rowptr[v + 1] - rowptr[v]);
+        if constexpr (COUNT) atomicAdd(&E[k], deg);
+        app = atomicExch(&stamp[v], epoch) != epoch;
+      }
+    }
+    const uint32_t pos = wave_append(app, &ctr->fl2);
+    if (app) fl[pos] = v;
+    wave_sum_add(app ? deg : 0ull, &ctr->ef2);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// top-down expand: edge-parallel over the frontier (load-balanced search on offs = inclusive
+// degree prefix). DIFF=true: frontier bits = visCur & ~visOld (frontier came from bottom-up);
+// DIFF=false: frontier bits are in accCur (frontier came from top-down / init).
+// ---------------------------------------------------------------------------------------------
+template <int W, bool DIFF>
+__global__ __launch_bounds__(kBlock) void k_td_expand(
+    const int32_t* fl, int64_t nf, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* visCur, const uint64_t* fsrc, const uint32_t* done, uint64_t* accNext,
+    int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int64_t total = offs[nf - 1];
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t eb = wave * VPW; eb < total; eb += nwaves * VPW) {
+    const int64_t e = eb + sub;
+    bool touch = false;
+    int32_t v = 0;
+    if (e < total) {
+      const int64_t i = upper_bound_i64(offs, nf, e);
+      const int32_t u = fl[i];
+      const int64_t start = i ? offs[i - 1] : 0;
+      v = col[rowptr[u] + (e - start)];
+      if (!is_done(done, v)) {
+        const int64_t uo = (int64_t)u * W + slot * VW, vo = (int64_t)v * W + slot * VW;
+        V<VW> fb = ldv<VW>(visCur + uo);
+        if constexpr (DIFF) {
+          const V<VW> old = ldv<VW>(fsrc + uo);
+#pragma unroll
+          for (int j = 0; j < VW; ++j) fb.w[j] &= ~old.w[j];
+        } else {
+          fb = ldv<VW>(fsrc + uo);
+        }
+        const V<VW> r = ldv<VW>(visCur + vo);
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          const uint64_t mm = fb.w[j] & ~r.w[j];
+          if (mm) {
+            atomicOr((unsigned long long*)&accNext[vo + j], mm);
+            any = true;
+          }
+        }
+        // one lane per group decides the first touch of v in this level
+        const uint64_t gm = (__ballot(any) >> (sub * G)) & L::GBITS;
+        if (gm && slot == 0) touch = atomicExch(&stamp[v], epoch) != epoch;
+      }
+    }
+    const uint32_t pos = wave_append(touch, &ctr->touched);
+    if (touch) touched[pos] = v;
+  }
+}
+
+// top-down finalize: new = acc & ~vis; update both visited buffers; build the next frontier.
+template <int W, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_td_finalize(
+    const int32_t* touched, const int64_t* rowptr, uint64_t* visCur, uint64_t* visOld,
+    uint64_t* accNext, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* fl2,
+    Ctr* ctr, unsigned long long* F, unsigned long long* E, uint64_t* alive_next, uint32_t level,
+    const int32_t* fl_old, int64_t nf_old, uint64_t* accCur_zero) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
+  __shared__ Lds<W, COUNT> s;
+  lds_zero(s);
+  const int64_t nt = ctr->touched;  // written by k_td_expand (previous kernel on the stream)
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  V<VW> am, gm;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    am.w[j] = alive[slot * VW + j];
+    gm.w[j] = gmask[slot * VW + j];
+  }
+  for (int64_t b = wave * VPW; b < nt; b += nwaves * VPW) {
+    const int64_t idx = b + sub;
+    const bool valid = idx < nt;
+    int32_t v = 0;
+    bool anynew = false, notfull = false;
+    V<VW> nw = vzero<VW>();
+    uint32_t deg = 0;
+    if (valid) {
+      v = touched[idx];
+      const int64_t vo = (int64_t)v * W + slot * VW;
+      const V<VW> a = ldv<VW>(accNext + vo);
+      const V<VW> r = ldv<VW>(visCur + vo);
+      V<VW> nv;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        nw.w[j] = a.w[j] & ~r.w[j];
+        nv.w[j] = r.w[j] | nw.w[j];
+        anynew |= nw.w[j] != 0;
+        notfull |= (~nv.w[j] & am.w[j] & gm.w[j]) != 0;
+      }
+      stv<VW>(accNext + vo, nw);
+      stv<VW>(visCur + vo, nv);
+      stv<VW>(visOld + vo, nv);
+      deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
+    }
+    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
+    const bool g_new = (bn >> (sub * G)) & L::GBITS;
+    const bool g_full = !((bf >> (sub * G)) & L::GBITS);
+    const bool leader = valid && slot == 0;
+    if (leader && g_full) set_done(done, v);
+    const bool app = leader && g_new;
+    const uint32_t pos = wave_append(app, &ctr->fl2);
+    if (app) fl2[pos] = v;
+    wave_sum_add(app ? (unsigned long long)deg : 0ull, &ctr->ef2);
+    if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
+  }
+  // zero the consumed top-down frontier bits of the previous frontier
+  if (accCur_zero) {
+    for (int64_t b = wave * VPW; b < nf_old; b += nwaves * VPW) {
+      const int64_t idx = b + sub;
+      if (idx < nf_old) stv<VW>(accCur_zero + (int64_t)fl_old[idx] * W + slot * VW, vzero<VW>());
+    }
+  }
+  lds_flush<W, COUNT>(s, F, E, alive_next, level);
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_zero_acc(const int32_t* fl, int64_t nf, uint64_t* acc) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = t; i < nf * G; i += stride) {
+    const int64_t idx = i / G;
+    const int slot = (int)(i % G);
+    stv<VW>(acc + (int64_t)fl[idx] * W + slot * VW, vzero<VW>());
+  }
+}
+
+// build the bottom-up active lists (deg > 0, not done), split by degree
+__global__ __launch_bounds__(kBlock) void k_build_active(int64_t n, const int64_t* rowptr,
+                                                         const uint32_t* done, int wide_deg,
+                                                         int32_t* act, int32_t* actw, Ctr* ctr) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t lim = (n + stride - 1) / stride * stride;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
+    int64_t d = 0;
+    bool ok = false;
+    if (i < n) {
+      d = rowptr[i + 1] - rowptr[i];
+      ok = d > 0 && !is_done(done, (int32_t)i);
+    }
+    const bool w = ok && d > wide_deg, nrw = ok && d <= wide_deg;
+    const uint32_t p1 = wave_append(nrw, &ctr->act2);
+    const uint32_t p2 = wave_append(w, &ctr->actw2);
+    if (nrw) act[p1] = (int32_t)i;
+    if (w) actw[p2] = (int32_t)i;
+    wave_sum_add(ok ? (unsigned long long)d : 0ull, &ctr->eu2);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// bottom-up, narrow vertices: G lanes per vertex, 4 neighbours in flight per lane, early exit
+// when every alive group is covered.
+// ---------------------------------------------------------------------------------------------
+template <int W, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_bu_narrow(
+    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
+    int32_t* act2, int32_t* fl2, Ctr* ctr, unsigned long long* F, unsigned long long* E,
+    uint64_t* alive_next, uint32_t level) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
+  __shared__ Lds<W, COUNT> s;
+  lds_zero(s);
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  for (int64_t b = wave * VPW; b < nact; b += nwaves * VPW) {
+    const int64_t idx = b + sub;
+    const bool valid = idx < nact;
+    int32_t v = 0;
+    V<VW> r = vzero<VW>(), unv = vzero<VW>(), acc = vzero<VW>();
+    bool lane_open = false;
+    int64_t beg = 0, end = 0;
+    if (valid) {
+      v = act[idx];
+      r = ldv<VW>(R + (int64_t)v * W + slot * VW);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        unv.w[j] = ~r.w[j] & am.w[j];
+        lane_open |= unv.w[j] != 0;
+      }
+      beg = rowptr[v];
+      end = rowptr[v + 1];
+    }
+    const bool g_open = valid && ((__ballot(lane_open) >> (sub * G)) & L::GBITS);
+    if (g_open) {
+      int64_t e = beg;
+      while (e < end) {
+        int32_t u[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) u[q] = (e + q < end) ? col[e + q] : -1;
+        V<VW> x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          x[q] = u[q] >= 0 ? ldv<VW>(R + (int64_t)u[q] * W + slot * VW) : vzero<VW>();
+        bool cov = true;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          acc.w[j] |= (x[0].w[j] | x[1].w[j] | x[2].w[j] | x[3].w[j]);
+          cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
+        }
+        e += 4;
+        // the whole group runs this loop in lock step (same v); exit when all lanes covered
+        if (!((__ballot(!cov) >> (sub * G)) & L::GBITS)) break;
+      }
+    }
+    V<VW> nw;
+    bool anynew = false, notfull = false;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      nw.w[j] = acc.w[j] & unv.w[j];
+      anynew |= nw.w[j] != 0;
+      notfull |= (unv.w[j] & ~nw.w[j]) != 0;
+    }
+    if (g_open) {
+      V<VW> nv;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
+      stv<VW>(Wb + (int64_t)v * W + slot * VW, nv);
+    }
+    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
+    const bool g_new = (bn >> (sub * G)) & L::GBITS;
+    const bool g_nf = (bf >> (sub * G)) & L::GBITS;
+    const bool leader = valid && slot == 0;
+    const uint32_t deg = (uint32_t)(end - beg);
+    if (leader && !g_nf) set_done(done, v);
+    const bool keep = leader && g_nf;
+    const uint32_t p1 = wave_append(keep, &ctr->act2);
+    if (keep) act2[p1] = v;
+    wave_sum_add(keep ? (unsigned long long)deg : 0ull, &ctr->eu2);
+    const bool app = leader && g_new;
+    const uint32_t p2 = wave_append(app, &ctr->fl2);
+    if (app) fl2[p2] = v;
+    wave_sum_add(app ? (unsigned long long)deg : 0ull, &ctr->ef2);
+    if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
+  }
+  lds_flush<W, COUNT>(s, F, E, alive_next, level);
+}
+
+// bottom-up, wide vertices: one wave per vertex; S = 64/G sub-groups stride the neighbour list
+// and OR-reduce across sub-groups once per 4*S neighbours for the early-exit test.
+template <int W, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_bu_wide(
+    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
+    int32_t* act2, int32_t* fl2, Ctr* ctr, unsigned long long* F, unsigned long long* E,
+    uint64_t* alive_next, uint32_t level) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, S = L::VPW;
+  __shared__ Lds<W, COUNT> s;
+  lds_zero(s);
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  for (int64_t idx = wave; idx < nact; idx += nwaves) {
+    const int32_t v = act[idx];
+    const V<VW> r = ldv<VW>(R + (int64_t)v * W + slot * VW);
+    V<VW> unv, acc = vzero<VW>();
+    bool lane_open = false;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      unv.w[j] = ~r.w[j] & am.w[j];
+      lane_open |= unv.w[j] != 0;
+    }
+    const bool open = __ballot(lane_open) != 0;
+    const int64_t beg = rowptr[v], end = rowptr[v + 1];
+    if (open) {
+      for (int64_t e0 = beg; e0 < end; e0 += 4 * S) {
+        int32_t u[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t e = e0 + sub + (int64_t)q * S;
+          u[q] = e < end ? col[e] : -1;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (u[q] >= 0) {
+            const V<VW> x = ldv<VW>(R + (int64_t)u[q] * W + slot * VW);
+#pragma unroll
+            for (int j = 0; j < VW; ++j) acc.w[j] |= x.w[j];
+          }
+        // OR-reduce across sub-groups (lane bits >= log2 G)
+#pragma unroll
+        for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+          for (int j = 0; j < VW; ++j) acc.w[j] |= __shfl_xor(acc.w[j], off);
+        bool cov = true;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
+        if (!__ballot(!cov)) break;
+      }
+    }
+    V<VW> nw;
+    bool anynew = false, notfull = false;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      nw.w[j] = acc.w[j] & unv.w[j];
+      anynew |= nw.w[j] != 0;
+      notfull |= (unv.w[j] & ~nw.w[j]) != 0;
+    }
+    if (open && sub == 0) {
+      V<VW> nv;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
+      stv<VW>(Wb + (int64_t)v * W + slot * VW, nv);
+    }
+    const bool g_new = __ballot(anynew) != 0;
+    const bool g_nf = __ballot(notfull) != 0;
+    const uint32_t deg = (uint32_t)(end - beg);
+    if (lane == 0) {
+      if (!g_nf) set_done(done, v);
+      else {
+        act2[atomicAdd(&ctr->actw2, 1u)] = v;
+        atomicAdd(&ctr->eu2, (unsigned long long)deg);
+      }
+      if (g_new) {
+        fl2[atomicAdd(&ctr->fl2, 1u)] = v;
+        atomicAdd(&ctr->ef2, (unsigned long long)deg);
+      }
+    }
+    if (anynew && sub == 0) count_bits<W, COUNT>(s, nw, slot, deg);
+  }
+  lds_flush<W, COUNT>(s, F, E, alive_next, level);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------------------------
+class BitparSolver final : public Solver {
+ public:
+  BitparSolver(const DeviceGraph& g, int max_groups) : g_(g) {
+    int w = 1;
+    while (w * 64 < max_groups && w < 16) w <<= 1;
+    maxW_ = w;
+    const int64_t n = std::max<int64_t>(g.n, 1);
+    const size_t vb = (size_t)n * maxW_ * sizeof(uint64_t);
+    for (int i = 0; i < 2; ++i) {
+      vis_[i].alloc(vb);
+      acc_[i].alloc(vb);
+      MSBFS_HIP_CHECK(hipMemset(acc_[i].p, 0, vb));
+    }
+    stamp_.alloc((size_t)n * sizeof(int32_t));
+    MSBFS_HIP_CHECK(hipMemset(stamp_.p, 0xFF, stamp_.bytes));
+    done_.alloc((size_t)((n + 31) / 32) * sizeof(uint32_t));
+    for (int i = 0; i < 2; ++i) {
+      act_[i].alloc((size_t)n * sizeof(int32_t));
+      actw_[i].alloc((size_t)n * sizeof(int32_t));
+      fl_[i].alloc((size_t)n * sizeof(int32_t));
+    }
+    touched_.alloc((size_t)n * sizeof(int32_t));
+    offs_.alloc((size_t)n * sizeof(int64_t));
+    scan_bytes_ = frontier_scan_temp_bytes(n);
+    scan_tmp_.alloc(scan_bytes_);
+    ctr_.alloc(sizeof(Ctr));
+    small_.alloc(64 * 16 * sizeof(unsigned long long) * 2 + 4 * 16 * sizeof(uint64_t));
+    hctr_ = std::make_unique<PinnedBuf>(sizeof(Ctr));
+    MSBFS_HIP_CHECK(hipDeviceSynchronize());
+  }
+
+  void run(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t* F, int64_t* edges2,
+           RunStats* st, hipStream_t stream) override {
+    int64_t k0 = 0;
+    while (k0 < K) {
+      int64_t remain = K - k0;
+      int w = 1;
+      while (w * 64 < remain && w < std::min(maxW_, opt.max_words)) w <<= 1;
+      const int64_t nb = std::min<int64_t>(remain, 64 * w);
+      run_batch(w, k0, nb, qoff, qids, F + k0, edges2 ? edges2 + k0 : nullptr, st, stream);
+      k0 += nb;
+      if (st) st->batches++;
+    }
+  }
+
+ private:
+  template <int W, bool COUNT>
+  void batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids, int64_t* F,
+                  int64_t* edges2, RunStats* st, hipStream_t s);
+
+  void run_batch(int w, int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
+                 int64_t* F, int64_t* edges2, RunStats* st, hipStream_t s) {
+    const bool c = edges2 != nullptr || opt.count_edges;
+#define MSBFS_BP_CASE(WW)                                                   \
+  case WW:                                                                  \
+    if (c) batch_impl<WW, true>(k0, nb, qoff, qids, F, edges2, st, s);      \
+    else batch_impl<WW, false>(k0, nb, qoff, qids, F, edges2, st, s);       \
+    break;
+    switch (w) {
+      MSBFS_BP_CASE(1)
+      MSBFS_BP_CASE(2)
+      MSBFS_BP_CASE(4)
+      MSBFS_BP_CASE(8)
+      MSBFS_BP_CASE(16)
+      default: fail("bad word count");
+    }
+#undef MSBFS_BP_CASE
+  }
+
+  Ctr read_ctr(hipStream_t s) {
+    MSBFS_HIP_CHECK(hipMemcpyAsync(hctr_->p, ctr_.p, sizeof(Ctr), hipMemcpyDeviceToHost, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    Ctr c;
+    std::memcpy(&c, hctr_->p, sizeof(Ctr));
+    return c;
+  }
+
+  const DeviceGraph& g_;
+  int maxW_ = 1;
+  DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
+      ctr_, small_, pairs_;
+  size_t scan_bytes_ = 0;
+  std::unique_ptr<PinnedBuf> hctr_;
+  int32_t epoch_ = 0;
+};
+
+template <int W, bool COUNT>
+void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
+                              int64_t* Fout, int64_t* edges2, RunStats* st, hipStream_t s) {
+  const int64_t n = g_.n;
+  const size_t vb = (size_t)std::max<int64_t>(n, 1) * W * sizeof(uint64_t);
+  // ---- per-batch state reset
+  MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));
+  MSBFS_HIP_CHECK(hipMemsetAsync(vis_[1].p, 0, vb, s));
+  MSBFS_HIP_CHECK(hipMemsetAsync(done_.p, 0, done_.bytes, s));
+  MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
+  MSBFS_HIP_CHECK(hipMemsetAsync(small_.p, 0, small_.bytes, s));
+  unsigned long long* dF = small_.as<unsigned long long>();
+  unsigned long long* dE = dF + 64 * 16;
+  uint64_t* alive[2] = {(uint64_t*)(dE + 64 * 16), (uint64_t*)(dE + 64 * 16) + 16};
+  uint64_t* gmask = alive[1] + 16;
+  {
+    uint64_t hm[16] = {0};
+    for (int64_t k = 0; k < nb; ++k) hm[k >> 6] |= 1ull << (k & 63);
+    MSBFS_HIP_CHECK(hipMemcpyAsync(gmask, hm, sizeof(hm), hipMemcpyHostToDevice, s));
+  }
+  // ---- sources: (vertex, local group) pairs, out-of-range ids dropped (main.cu:49)
+  std::vector<int32_t> hp;
+  hp.reserve(2 * (qoff[k0 + nb] - qoff[k0]));
+  std::vector<int32_t> hk;
+  for (int64_t k = 0; k < nb; ++k)
+    for (int64_t j = qoff[k0 + k]; j < qoff[k0 + k + 1]; ++j) {
+      const int32_t v = qids[j];
+      if (v >= 0 && v < n) {
+        hp.push_back(v);
+        hk.push_back((int32_t)k);
+      }
+    }
+  const int64_t np = (int64_t)hp.size();
+  pairs_.ensure((size_t)std::max<int64_t>(np, 1) * 2 * sizeof(int32_t));
+  int32_t* dpv = pairs_.as<int32_t>();
+  int32_t* dpk = dpv + std::max<int64_t>(np, 1);
+  hp.insert(hp.end(), hk.begin(), hk.end());
+  if (np) {
+    MSBFS_HIP_CHECK(hipMemcpyAsync(dpv, hp.data(), np * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(dpk, hp.data() + np, np * sizeof(int32_t),
+                                   hipMemcpyHostToDevice, s));
+  }
+  int cur = 0;  // vis_[cur] = read buffer (up to date for every non-done vertex)
+  int fc = 0;   // fl_[fc] = current frontier
+  int ac = 0;   // acc_[ac] holds the current frontier bits when fsrc_acc
+  ++epoch_;
+  if (np) {
+    k_init<W, COUNT><<<grid_for(np, kBlock), kBlock, 0, s>>>(
+        dpv, dpk, np, g_.rowptr, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
+        acc_[ac].as<uint64_t>(), stamp_.as<int32_t>(), epoch_, fl_[fc].as<int32_t>(),
+        ctr_.as<Ctr>(), dE, alive[0]);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  Ctr c = read_ctr(s);
+  int64_t nf = c.fl2, ef = (int64_t)c.ef2;
+  int64_t na = n, ea = g_.nnz;  // active estimate before the first bottom-up build
+  int64_t nact = 0, nactw = 0;
+  bool have_active = false, fsrc_acc = true, bottom_up = false;
+  int alv = 0;
+  uint32_t level = 0;
+  const int grid = 2048;
+  while (nf > 0) {
+    // direction choice (Beamer et al. SC'12, on the union frontier)
+    if (opt.force_dir == 1) bottom_up = false;
+    else if (opt.force_dir == 2) bottom_up = level > 0;
+    else if (!bottom_up) bottom_up = (double)ef > (double)ea / opt.alpha;
+    else bottom_up = !((double)nf < (double)na / opt.beta && (double)ef < (double)ea / opt.alpha);
+    MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
+    MSBFS_HIP_CHECK(hipMemsetAsync(alive[alv ^ 1], 0, 16 * sizeof(uint64_t), s));
+    ++level;
+    uint64_t* R = vis_[cur].as<uint64_t>();
+    uint64_t* O = vis_[cur ^ 1].as<uint64_t>();
+    if (!bottom_up) {
+      // ---- top-down
+      frontier_degree_scan(g_.rowptr, fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(),
+                           scan_tmp_.p, scan_bytes_, s);
+      ++epoch_;
+      const int64_t groups = (ef + Lay<W>::VPW - 1) / Lay<W>::VPW;
+      const int eg = grid_for(groups, kBlock / 64, 8192);
+      if (fsrc_acc)
+        k_td_expand<W, false><<<eg, kBlock, 0, s>>>(
+            fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
+            acc_[ac].as<uint64_t>(), done_.as<uint32_t>(), acc_[ac ^ 1].as<uint64_t>(),
+            stamp_.as<int32_t>(), epoch_, touched_.as<int32_t>(), ctr_.as<Ctr>());
+      else
+        k_td_expand<W, true><<<eg, kBlock, 0, s>>>(
+            fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R, O,
+            done_.as<uint32_t>(), acc_[ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
+            touched_.as<int32_t>(), ctr_.as<Ctr>());
+      MSBFS_HIP_CHECK(hipGetLastError());
+      // touched <= min(n, frontier edges); the kernel reads the exact count from ctr
+      const int64_t nt_max = std::min<int64_t>(std::max<int64_t>(ef, nf), n);
+      k_td_finalize<W, COUNT><<<grid_for(nt_max, kBlock / 64 * Lay<W>::VPW, grid), kBlock, 0, s>>>(
+          touched_.as<int32_t>(), g_.rowptr, R, O, acc_[ac ^ 1].as<uint64_t>(), alive[alv],
+          gmask, done_.as<uint32_t>(), fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), dF, dE,
+          alive[alv ^ 1], level, fl_[fc].as<int32_t>(), nf,
+          fsrc_acc ? acc_[ac].as<uint64_t>() : nullptr);
+      MSBFS_HIP_CHECK(hipGetLastError());
+      ac ^= 1;
+      fsrc_acc = true;
+      if (st) st->td_levels++;
+    } else {
+      // ---- bottom-up
+      if (!have_active) {
+        MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
+        k_build_active<<<grid_for(n, kBlock), kBlock, 0, s>>>(
+            n, g_.rowptr, done_.as<uint32_t>(), opt.wide_degree, act_[0].as<int32_t>(),
+            actw_[0].as<int32_t>(), ctr_.as<Ctr>());
+        MSBFS_HIP_CHECK(hipGetLastError());
+        c = read_ctr(s);
+        nact = c.act2;
+        nactw = c.actw2;
+        have_active = true;
+        MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
+      }
+      if (fsrc_acc) {
+        // bottom-up does not read frontier bits; clear the pending top-down ones
+        k_zero_acc<W><<<grid_for(nf * Lay<W>::G, kBlock), kBlock, 0, s>>>(
+            fl_[fc].as<int32_t>(), nf, acc_[ac].as<uint64_t>());
+        MSBFS_HIP_CHECK(hipGetLastError());
+      }
+      if (nact)
+        k_bu_narrow<W, COUNT><<<grid_for(nact, kBlock / 64 * Lay<W>::VPW, grid), kBlock, 0, s>>>(
+            act_[0].as<int32_t>(), nact, g_.rowptr, g_.col, R, O, alive[alv], gmask,
+            done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
+            ctr_.as<Ctr>(), dF, dE, alive[alv ^ 1], level);
+      if (nactw)
+        k_bu_wide<W, COUNT><<<grid_for(nactw, kBlock / 64, grid), kBlock, 0, s>>>(
+            actw_[0].as<int32_t>(), nactw, g_.rowptr, g_.col, R, O, alive[alv], gmask,
+            done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
+            ctr_.as<Ctr>(), dF, dE, alive[alv ^ 1], level);
+      MSBFS_HIP_CHECK(hipGetLastError());
+      std::swap(act_[0], act_[1]);
+      std::swap(actw_[0], actw_[1]);
+      cur ^= 1;
+      fsrc_acc = false;
+      if (st) st->bu_levels++;
+    }
+    c = read_ctr(s);
+    if (bottom_up) {
+      nact = c.act2;
+      nactw = c.actw2;
+      na = nact + nactw;
+      ea = (int64_t)c.eu2;
+    }
+    nf = c.fl2;
+    ef = (int64_t)c.ef2;
+    fc ^= 1;
+    alv ^= 1;
+    if (st) st->levels++;
+  }
+  // frontier is empty: accumulator entries were cleared by finalize / zero_acc
+  std::vector<unsigned long long> hF(64 * 16), hE(64 * 16);
+  MSBFS_HIP_CHECK(hipMemcpyAsync(hF.data(), dF, 64 * 16 * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, s));
+  if (edges2)
+    MSBFS_HIP_CHECK(hipMemcpyAsync(hE.data(), dE, 64 * 16 * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  for (int64_t k = 0; k < nb; ++k) {
+    Fout[k] = (int64_t)hF[k];
+    if (edges2) edges2[k] = (int64_t)hE[k];
+  }
+}
+
+}  // namespace bp
+
+std::unique_ptr<Solver> make_bitpar_solver(const DeviceGraph& g, int max_groups) {
+  return std::make_unique<bp::BitparSolver>(g, max_groups);
+}
+
+}  // namespace msbfs

@@ -1,0 +1,351 @@
+// Device graph construction: RMAT / uniform generation and count -> scan -> scatter CSR build.
+//
+// The reference builds the CSR serially on rank 0 from a vector<vector<int>> (main.cu:106-129)
+// and broadcasts it through host MPI (main.cu:241-255). Here every GPU can build its own replica
+// straight in HBM: the counter-based generator (common.hpp) is evaluated twice — once to count
+// degrees, once to scatter — so no edge list is ever materialised (RMAT-30's 137 GB edge list
+// would not fit next to its CSR). int64 offsets lift the reference's 2m <= INT_MAX limit.
+#include <hipcub/hipcub.hpp>
+
+#include "msbfs/device.hpp"
+
+namespace msbfs {
+namespace {
+
+constexpr int kBlock = 256;
+
+__global__ __launch_bounds__(kBlock) void k_rmat_pass(RmatParams p, int64_t m,
+                                                      unsigned long long* cnt, int32_t* col,
+                                                      int scatter) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    uint32_t u, v;
+    rmat_edge(p, (uint64_t)i, u, v);
+    if (!scatter) {
+      atomicAdd(&cnt[u], 1ull);
+      atomicAdd(&cnt[v], 1ull);
+    } else {
+      col[atomicAdd(&cnt[u], 1ull)] = (int32_t)v;
+      col[atomicAdd(&cnt[v], 1ull)] = (int32_t)u;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_uniform_pass(uint64_t seed, int64_t n, int64_t m,
+                                                         unsigned long long* cnt, int32_t* col,
+                                                         int scatter) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    uint32_t u, v;
+    uniform_edge(seed, (uint64_t)i, (uint64_t)n, u, v);
+    if (!scatter) {
+      atomicAdd(&cnt[u], 1ull);
+      atomicAdd(&cnt[v], 1ull);
+    } else {
+      col[atomicAdd(&cnt[u], 1ull)] = (int32_t)v;
+      col[atomicAdd(&cnt[v], 1ull)] = (int32_t)u;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_edges_pass(const int32_t* eu, const int32_t* ev,
+                                                       int64_t m, unsigned long long* cnt,
+                                                       int32_t* col, int scatter) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    const int32_t u = eu[i], v = ev[i];
+    if (!scatter) {
+      atomicAdd(&cnt[u], 1ull);
+      atomicAdd(&cnt[v], 1ull);
+    } else {
+      col[atomicAdd(&cnt[u], 1ull)] = v;
+      col[atomicAdd(&cnt[v], 1ull)] = u;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy_i64(const int64_t* src, int64_t* dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_degree_stats(const int64_t* rowptr, int64_t n,
+                                                         unsigned long long* out /*max, iso*/) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long mx = 0, iso = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const unsigned long long d = (unsigned long long)(rowptr[i + 1] - rowptr[i]);
+    mx = d > mx ? d : mx;
+    iso += d == 0;
+  }
+  // wave64 reduction then one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long om = __shfl_xor(mx, off);
+    mx = om > mx ? om : mx;
+    iso += __shfl_xor(iso, off);
+  }
+  if (lane_id() == 0) {
+    atomicMax(&out[0], mx);
+    atomicAdd(&out[1], iso);
+  }
+}
+
+// Per-row sort of neighbour lists: rows up to 1024 entries are bitonic-sorted in LDS by one
+// block; longer rows by a per-row radix sort pass in chunks (rare: only hubs).
+template <int CAP>
+__global__ __launch_bounds__(256) void k_sort_rows_lds(const int64_t* rowptr, int32_t* col,
+                                                      const int32_t* rows, int64_t nrows) {
+  __shared__ int32_t s[CAP];
+  for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const int32_t v = rows[r];
+    const int64_t b = rowptr[v];
+    const int len = (int)(rowptr[v + 1] - b);
+    for (int i = threadIdx.x; i < CAP; i += blockDim.x) s[i] = i < len ? col[b + i] : INT32_MAX;
+    __syncthreads();
+    for (int k = 2; k <= CAP; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < CAP; i += blockDim.x) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const int32_t a = s[i], c = s[ixj];
+            const bool up = (i & k) == 0;
+            if ((a > c) == up) { s[i] = c; s[ixj] = a; }
+          }
+        }
+        __syncthreads();
+      }
+    for (int i = threadIdx.x; i < len; i += blockDim.x) col[b + i] = s[i];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bucket_rows(const int64_t* rowptr, int64_t n,
+                                                        int32_t* small, uint32_t* nsmall,
+                                                        int32_t* mid, uint32_t* nmid,
+                                                        int32_t* big, uint32_t* nbig) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t lim = (n + stride - 1) / stride * stride;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
+    const int64_t d = i < n ? rowptr[i + 1] - rowptr[i] : 0;
+    const bool a = d > 1 && d <= 64, bm = d > 64 && d <= 1024, c = d > 1024;
+    const uint32_t pa = wave_append(a, nsmall);
+    const uint32_t pb = wave_append(bm, nmid);
+    const uint32_t pc = wave_append(c, nbig);
+    if (a) small[pa] = (int32_t)i;
+    if (bm) mid[pb] = (int32_t)i;
+    if (c) big[pc] = (int32_t)i;
+  }
+}
+
+// one lane per row, insertion sort (rows <= 64)
+__global__ __launch_bounds__(kBlock) void k_sort_rows_small(const int64_t* rowptr, int32_t* col,
+                                                           const int32_t* rows, int64_t nrows) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows; r += stride) {
+    const int32_t v = rows[r];
+    int32_t* a = col + rowptr[v];
+    const int len = (int)(rowptr[v + 1] - rowptr[v]);
+    for (int i = 1; i < len; ++i) {
+      const int32_t x = a[i];
+      int j = i - 1;
+      while (j >= 0 && a[j] > x) { a[j + 1] = a[j]; --j; }
+      a[j + 1] = x;
+    }
+  }
+}
+
+void build_from_counts(DeviceGraph& g, DevBuf& cnt, hipStream_t s) {
+  // cnt[0..n) holds degrees (int64). rowptr[0]=0, rowptr[1..n] = inclusive scan.
+  const int64_t n = g.n;
+  MSBFS_HIP_CHECK(hipMemsetAsync(g.rowptr, 0, sizeof(int64_t), s));
+  size_t tb = 0;
+  MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, cnt.as<int64_t>(), g.rowptr + 1,
+                                                   (int)n, s));
+  DevBuf tmp(tb);
+  MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, cnt.as<int64_t>(), g.rowptr + 1,
+                                                   (int)n, s));
+  int64_t nnz = 0;
+  MSBFS_HIP_CHECK(hipMemcpyAsync(&nnz, g.rowptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  g.nnz = nnz;
+  // cursor := rowptr[0..n)
+  k_copy_i64<<<grid_for(n, kBlock), kBlock, 0, s>>>(g.rowptr, cnt.as<int64_t>(), n);
+  MSBFS_HIP_CHECK(hipGetLastError());
+  g.own_col.alloc((size_t)std::max<int64_t>(nnz, 1) * sizeof(int32_t));
+  g.col = g.own_col.as<int32_t>();
+}
+
+void alloc_rowptr(DeviceGraph& g, int64_t n) {
+  if (n < 0 || n > INT32_MAX) fail("vertex count must fit int32 ids");
+  g.n = n;
+  g.own_rowptr.alloc((size_t)(n + 1) * sizeof(int64_t));
+  g.rowptr = g.own_rowptr.as<int64_t>();
+}
+
+}  // namespace
+
+void device_graph_stats(DeviceGraph& g, hipStream_t s) {
+  DevBuf out(2 * sizeof(unsigned long long));
+  MSBFS_HIP_CHECK(hipMemsetAsync(out.p, 0, out.bytes, s));
+  if (g.n > 0) {
+    k_degree_stats<<<grid_for(g.n, kBlock), kBlock, 0, s>>>(g.rowptr, g.n,
+                                                          out.as<unsigned long long>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  unsigned long long h[2];
+  MSBFS_HIP_CHECK(hipMemcpyAsync(h, out.p, sizeof(h), hipMemcpyDeviceToHost, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  g.max_degree = (int64_t)h[0];
+  g.isolated = (int64_t)h[1];
+}
+
+void device_graph_from_host(DeviceGraph& g, int64_t n, const int64_t* rowptr, const int32_t* col,
+                            hipStream_t s) {
+  alloc_rowptr(g, n);
+  g.nnz = rowptr[n];
+  g.m = g.nnz / 2;
+  g.own_col.alloc((size_t)std::max<int64_t>(g.nnz, 1) * sizeof(int32_t));
+  g.col = g.own_col.as<int32_t>();
+  MSBFS_HIP_CHECK(hipMemcpyAsync(g.rowptr, rowptr, (n + 1) * sizeof(int64_t),
+                                 hipMemcpyHostToDevice, s));
+  if (g.nnz)
+    MSBFS_HIP_CHECK(hipMemcpyAsync(g.col, col, g.nnz * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  device_graph_stats(g, s);
+}
+
+void device_graph_from_edges(DeviceGraph& g, int64_t n, int64_t m, const int32_t* d_u,
+                             const int32_t* d_v, hipStream_t s) {
+  alloc_rowptr(g, n);
+  g.m = m;
+  DevBuf cnt((size_t)std::max<int64_t>(n, 1) * sizeof(int64_t));
+  MSBFS_HIP_CHECK(hipMemsetAsync(cnt.p, 0, cnt.bytes, s));
+  if (m) {
+    k_edges_pass<<<grid_for(m, kBlock), kBlock, 0, s>>>(d_u, d_v, m, cnt.as<unsigned long long>(),
+                                                       nullptr, 0);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  build_from_counts(g, cnt, s);
+  if (m) {
+    k_edges_pass<<<grid_for(m, kBlock), kBlock, 0, s>>>(d_u, d_v, m, cnt.as<unsigned long long>(),
+                                                       g.col, 1);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  device_graph_stats(g, s);
+}
+
+void device_graph_gen_rmat(DeviceGraph& g, int scale, int64_t edgefactor, uint64_t seed, double a,
+                           double b, double c, int scramble, hipStream_t s) {
+  if (scale < 1 || scale > 31) fail("rmat scale must be in [1, 31]");
+  const int64_t n = int64_t(1) << scale, m = n * edgefactor;
+  alloc_rowptr(g, n);
+  g.m = m;
+  const RmatParams p = make_rmat_params(scale, seed, a, b, c, scramble);
+  DevBuf cnt((size_t)n * sizeof(int64_t));
+  MSBFS_HIP_CHECK(hipMemsetAsync(cnt.p, 0, cnt.bytes, s));
+  const int grid = grid_for(m, kBlock, 8192);
+  k_rmat_pass<<<grid, kBlock, 0, s>>>(p, m, cnt.as<unsigned long long>(), nullptr, 0);
+  MSBFS_HIP_CHECK(hipGetLastError());
+  build_from_counts(g, cnt, s);
+  k_rmat_pass<<<grid, kBlock, 0, s>>>(p, m, cnt.as<unsigned long long>(), g.col, 1);
+  MSBFS_HIP_CHECK(hipGetLastError());
+  device_graph_stats(g, s);
+}
+
+void device_graph_gen_uniform(DeviceGraph& g, int64_t n, int64_t m, uint64_t seed, hipStream_t s) {
+  alloc_rowptr(g, n);
+  g.m = m;
+  DevBuf cnt((size_t)std::max<int64_t>(n, 1) * sizeof(int64_t));
+  MSBFS_HIP_CHECK(hipMemsetAsync(cnt.p, 0, cnt.bytes, s));
+  const int grid = grid_for(m, kBlock, 8192);
+  if (m) {
+    k_uniform_pass<<<grid, kBlock, 0, s>>>(seed, n, m, cnt.as<unsigned long long>(), nullptr, 0);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  build_from_counts(g, cnt, s);
+  if (m) {
+    k_uniform_pass<<<grid, kBlock, 0, s>>>(seed, n, m, cnt.as<unsigned long long>(), g.col, 1);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  device_graph_stats(g, s);
+}
+
+void device_graph_sort_rows(DeviceGraph& g, hipStream_t s) {
+  // Sorted rows make the device CSR deterministic (the atomic scatter is not) and give bottom-up
+  // sweeps ascending-id neighbour order. Rows > 1024 are sorted with a segmented radix sort.
+  const int64_t n = g.n;
+  if (n == 0) return;
+  DevBuf lists((size_t)3 * n * sizeof(int32_t)), cnts(4 * sizeof(uint32_t));
+  int32_t* small = lists.as<int32_t>();
+  int32_t* mid = small + n;
+  int32_t* big = mid + n;
+  uint32_t* c = cnts.as<uint32_t>();
+  MSBFS_HIP_CHECK(hipMemsetAsync(c, 0, cnts.bytes, s));
+  k_bucket_rows<<<grid_for(n, kBlock), kBlock, 0, s>>>(g.rowptr, n, small, c, mid, c + 1, big, c + 2);
+  MSBFS_HIP_CHECK(hipGetLastError());
+  uint32_t h[3];
+  MSBFS_HIP_CHECK(hipMemcpyAsync(h, c, sizeof(h), hipMemcpyDeviceToHost, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  if (h[0]) {
+    k_sort_rows_small<<<grid_for(h[0], kBlock), kBlock, 0, s>>>(g.rowptr, g.col, small, h[0]);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  if (h[1]) {
+    k_sort_rows_lds<1024><<<std::min<uint32_t>(h[1], 4096), 256, 0, s>>>(g.rowptr, g.col, mid, h[1]);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  if (h[2]) {
+    std::vector<int32_t> rows(h[2]);
+    MSBFS_HIP_CHECK(hipMemcpyAsync(rows.data(), big, h[2] * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    std::vector<int64_t> rp(n + 1);
+    MSBFS_HIP_CHECK(hipMemcpyAsync(rp.data(), g.rowptr, (n + 1) * sizeof(int64_t),
+                                   hipMemcpyDeviceToHost, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    DevBuf tmpkeys, temp;
+    for (int32_t v : rows) {
+      const int64_t b = rp[v], len = rp[v + 1] - rp[v];
+      tmpkeys.ensure(len * sizeof(int32_t));
+      size_t tb = 0;
+      MSBFS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, g.col + b,
+                                                        tmpkeys.as<int32_t>(), (int)len, 0, 32, s));
+      temp.ensure(tb);
+      MSBFS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, tb, g.col + b,
+                                                        tmpkeys.as<int32_t>(), (int)len, 0, 32, s));
+      MSBFS_HIP_CHECK(hipMemcpyAsync(g.col + b, tmpkeys.p, len * sizeof(int32_t),
+                                     hipMemcpyDeviceToDevice, s));
+    }
+  }
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+// ---- frontier degree scan (shared by the level loops) ----------------------------------------
+namespace {
+__global__ __launch_bounds__(kBlock) void k_list_degrees(const int64_t* rowptr, const int32_t* list,
+                                                         int64_t cnt, int64_t* out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += stride) {
+    const int32_t v = list[i];
+    out[i] = rowptr[v + 1] - rowptr[v];
+  }
+}
+}  // namespace
+
+size_t frontier_scan_temp_bytes(int64_t max_items) {
+  size_t tb = 0;
+  MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, (int64_t*)nullptr,
+                                                   (int64_t*)nullptr, (int)std::max<int64_t>(max_items, 1)));
+  return tb + (size_t)std::max<int64_t>(max_items, 1) * sizeof(int64_t) + 256;
+}
+
+void frontier_degree_scan(const int64_t* rowptr, const int32_t* list, int64_t cnt, int64_t* offs,
+                          void* temp, size_t temp_bytes, hipStream_t s) {
+  if (cnt <= 0) return;
+  int64_t* degs = (int64_t*)temp;
+  char* t2 = (char*)temp + (((size_t)cnt * sizeof(int64_t) + 255) & ~size_t(255));
+  size_t tb = temp_bytes - ((size_t)(t2 - (char*)temp));
+  k_list_degrees<<<grid_for(cnt, kBlock), kBlock, 0, s>>>(rowptr, list, cnt, degs);
+  MSBFS_HIP_CHECK(hipGetLastError());
+  MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(t2, tb, degs, offs, (int)cnt, s));
+}
+
+}  // namespace msbfs

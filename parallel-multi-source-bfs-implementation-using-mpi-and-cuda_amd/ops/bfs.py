@@ -1,0 +1,118 @@
+"""Multi-source BFS operators: F(U_k) for every query group.
+
+F(U) = sum over vertices v reachable from U of dist(U, v) (reference GPUMultiSourceBFS +
+ComputeFofU, main.cu:40-89). Sources outside [0, n) are ignored (main.cu:49); unreachable
+vertices contribute nothing (main.cu:84-85).
+
+Algorithms (all give identical F — it is an exact integer sum):
+  bitpar  — 64*W groups per pass, direction-optimising, per-group sums on chip (default, K > 1)
+  dist    — per-group distance array, direction-optimising (default for K == 1)
+  topdown — per-group, top-down only (queue + load-balanced edge expansion)
+  sweep   — the reference algorithm (thread per vertex, full sweep per level), on-device sum
+  cpu     — host threads (query-parallel), the "serial CPU BFS" config and oracle
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional, Union
+
+import numpy as np
+
+from . import native
+from ..models.graph import DeviceGraph, Graph
+from ..models.queries import QuerySet
+
+
+@dataclass
+class BfsResult:
+    F: np.ndarray                      # int64[K]
+    edges: Optional[np.ndarray] = None  # int64[K], Graph500 traversed edges per group (if asked)
+    stats: dict = field(default_factory=dict)
+
+
+class Solver:
+    """Reusable device workspace for one graph + algorithm (allocated once, like the reference's
+    one-time cudaMalloc of the distance array main.cu:294-295, but for all algorithms)."""
+
+    def __init__(self, graph: DeviceGraph, algo: str = "auto", max_groups: int = 1024,
+                 alpha: float = 0.0, beta: float = 0.0, wide_degree: int = 0,
+                 force_dir: int = 0, max_words: int = 0):
+        if algo not in native.ALGOS or algo == "cpu":
+            raise ValueError(f"unknown device algorithm {algo!r}")
+        self.graph = graph
+        self.algo = algo
+        h = C.c_void_p()
+        native.check(native.lib().msbfs_solver_create(graph.handle, native.ALGOS[algo],
+                                                      max(1, int(max_groups)), C.byref(h)))
+        self._h = h
+        if alpha or beta or wide_degree or force_dir or max_words:
+            o = native.Options(alpha, beta, wide_degree, force_dir, max_words)
+            native.check(native.lib().msbfs_solver_set_options(self._h, C.byref(o)))
+
+    def run(self, queries: QuerySet, count_edges: bool = False, stream: Optional[int] = None
+            ) -> BfsResult:
+        K = queries.K
+        F = np.zeros(K, dtype=np.int64)
+        E = np.zeros(K, dtype=np.int64) if count_edges else None
+        st = native.Stats()
+        if K:
+            native.check(native.lib().msbfs_solver_run(
+                self._h, K, native.ptr(queries.off, C.c_int64), native.ptr(queries.ids, C.c_int32),
+                native.ptr(F, C.c_int64), native.ptr(E, C.c_int64) if E is not None else None,
+                C.byref(st), C.c_void_p(stream) if stream else None))
+        return BfsResult(F, None if E is None else E // 2, st.as_dict())
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            native.lib().msbfs_solver_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def cpu_bfs(graph: Graph, queries: QuerySet, threads: int = 0, count_edges: bool = False
+            ) -> BfsResult:
+    """Query-parallel host BFS (native C++ threads)."""
+    K = queries.K
+    F = np.zeros(K, dtype=np.int64)
+    E = np.zeros(K, dtype=np.int64) if count_edges else None
+    if K:
+        native.check(native.lib().msbfs_cpu_run(
+            graph.n, native.ptr(graph.rowptr, C.c_int64), native.ptr(graph.col, C.c_int32), K,
+            native.ptr(queries.off, C.c_int64), native.ptr(queries.ids, C.c_int32),
+            native.ptr(F, C.c_int64), native.ptr(E, C.c_int64) if E is not None else None,
+            int(threads)))
+    return BfsResult(F, E, {})
+
+
+def multi_source_bfs(graph: Union[Graph, DeviceGraph], queries: QuerySet, algo: str = "auto",
+                     device: int = 0, count_edges: bool = False, **opts) -> BfsResult:
+    """One-shot convenience wrapper (creates and frees a Solver)."""
+    if algo == "cpu":
+        if isinstance(graph, DeviceGraph):
+            graph = graph.download()
+        return cpu_bfs(graph, queries, count_edges=count_edges)
+    dg = graph if isinstance(graph, DeviceGraph) else DeviceGraph.from_host(graph, device)
+    with Solver(dg, algo, max_groups=max(1, queries.K), **opts) as s:
+        return s.run(queries, count_edges=count_edges)
+
+
+def argmin_first(F: np.ndarray) -> int:
+    """Reference tie-break (main.cu:381-397): first valid F, strict '<' => lowest index wins.
+    Returns -1 for K == 0."""
+    F = np.asarray(F)
+    valid = np.nonzero(F >= 0)[0]
+    if len(valid) == 0:
+        return -1
+    return int(valid[np.argmin(F[valid])])  # argmin returns the first minimum

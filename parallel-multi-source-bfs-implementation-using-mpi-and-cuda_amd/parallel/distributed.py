@@ -1,0 +1,250 @@
+"""Query-level data parallelism over torch.distributed (RCCL over xGMI on MI355X, gloo on CPU).
+
+Reference distributed layer: MPI_Bcast of n, m, row_offsets, col_indices
+(main.cu:242-255), 2K+1 MPI_Bcast for the queries (main.cu:257-280), static round-robin
+kidx = rank, rank+P, ... (main.cu:304-307), MPI_Gather + MPI_Gatherv of (q, F) pairs with a custom
+struct datatype (main.cu:324-368) and a serial argmin on rank 0 (main.cu:377-397).
+
+MI355X design:
+  * one process per GPU, `torch.distributed` with backend "nccl" (= RCCL);
+  * the CSR is broadcast HBM -> HBM (device tensors, chunked) — or not at all when every rank
+    generates the identical graph in its own HBM (deterministic counter-based generator);
+  * queries travel as ONE packed (off, ids) blob;
+  * the result is ONE 8-byte all-reduce(MIN) on a packed key (F << qbits | q): min F, and the
+    lowest query index among ties — exactly the reference's strict-'<' first-wins argmin.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+
+CHUNK_BYTES = 1 << 30
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: int = -1          # GPU ordinal, -1 for CPU
+    backend: str = "none"     # "nccl" (RCCL), "gloo" or "none" (single process)
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1 and self.backend != "none"
+
+    def torch_device(self):
+        import torch
+        return torch.device("cuda", self.device) if self.device >= 0 else torch.device("cpu")
+
+
+def init_from_env(backend: Optional[str] = None, gpus_per_node: Optional[int] = None,
+                  use_gpu: Optional[bool] = None) -> DistContext:
+    """Initialise from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
+
+    Device binding follows the reference: device = local_rank % gpus_per_node (main.cu:227).
+    """
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    device = -1
+    if use_gpu:
+        ngpu = torch.cuda.device_count()
+        per_node = gpus_per_node or ngpu
+        device = (local_rank % per_node) % max(ngpu, 1)
+        torch.cuda.set_device(device)
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    if world > 1:
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29500")
+            kw = {}
+            if backend == "nccl" and device >= 0:
+                kw["device_id"] = torch.device("cuda", device)
+            dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+        return DistContext(rank, world, local_rank, device, backend)
+    return DistContext(0, 1, 0, device, "none")
+
+
+def shutdown(ctx: DistContext) -> None:
+    import torch.distributed as dist
+    if ctx.distributed and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def round_robin(K: int, rank: int, world: int) -> np.ndarray:
+    """Static assignment of main.cu:304-307: kidx = rank, rank + world, ..."""
+    return np.arange(rank, K, world, dtype=np.int64)
+
+
+def _comm_device(ctx: DistContext):
+    import torch
+    return torch.device("cuda", ctx.device) if ctx.backend == "nccl" else torch.device("cpu")
+
+
+def barrier(ctx: DistContext) -> None:
+    import torch.distributed as dist
+    if ctx.distributed:
+        if ctx.backend == "nccl":
+            dist.barrier(device_ids=[ctx.device])
+        else:
+            dist.barrier()
+
+
+def broadcast_array(arr: Optional[np.ndarray], ctx: DistContext, dtype, count: int,
+                    root: int = 0) -> np.ndarray:
+    """Broadcast a host array from root (through device memory when the backend is RCCL)."""
+    import torch
+    import torch.distributed as dist
+
+    if not ctx.distributed:
+        return arr
+    out = arr if ctx.rank == root else np.empty(count, dtype=dtype)
+    dev = _comm_device(ctx)
+    elems = max(1, CHUNK_BYTES // np.dtype(dtype).itemsize)
+    for s in range(0, count, elems):
+        e = min(count, s + elems)
+        t = torch.from_numpy(np.ascontiguousarray(out[s:e])).to(dev)
+        dist.broadcast(t, src=root)
+        if ctx.rank != root:
+            out[s:e] = t.cpu().numpy()
+    return out
+
+
+def broadcast_tensor_(t, ctx: DistContext, root: int = 0):
+    """In-place chunked broadcast of a (device) tensor."""
+    import torch.distributed as dist
+    if not ctx.distributed:
+        return t
+    flat = t.view(-1)
+    elems = max(1, CHUNK_BYTES // t.element_size())
+    for s in range(0, flat.numel(), elems):
+        dist.broadcast(flat[s:s + elems], src=root)
+    return t
+
+
+def broadcast_header(vals: Tuple[int, ...], ctx: DistContext, root: int = 0) -> Tuple[int, ...]:
+    a = np.asarray(vals, dtype=np.int64) if ctx.rank == root else None
+    return tuple(int(x) for x in broadcast_array(a, ctx, np.int64, len(vals), root))
+
+
+def broadcast_queries(qs, ctx: DistContext, root: int = 0):
+    """One packed blob instead of 2K+1 broadcasts (main.cu:257-280)."""
+    from ..models.queries import QuerySet
+    if not ctx.distributed:
+        return qs
+    K, nids = broadcast_header((qs.K, len(qs.ids)) if ctx.rank == root else (0, 0), ctx, root)
+    off = broadcast_array(qs.off if ctx.rank == root else None, ctx, np.int64, K + 1, root)
+    ids = broadcast_array(qs.ids if ctx.rank == root else None, ctx, np.int32, nids, root)
+    return QuerySet(off, ids)
+
+
+def broadcast_graph(g, ctx: DistContext, root: int = 0):
+    """Replicate rank root's host Graph on every rank.
+
+    RCCL backend: returns (rowptr, col) *device tensors* broadcast HBM -> HBM over xGMI;
+    otherwise a host Graph. (The reference broadcasts pageable host vectors, main.cu:250,255.)
+    """
+    import torch
+    from ..models.graph import Graph
+
+    if not ctx.distributed:
+        return g
+    n, m, nnz = broadcast_header((g.n, g.m, g.nnz) if ctx.rank == root else (0, 0, 0), ctx, root)
+    if ctx.backend == "nccl":
+        dev = torch.device("cuda", ctx.device)
+        if ctx.rank == root:
+            rowptr = torch.from_numpy(g.rowptr).to(dev)
+            col = torch.from_numpy(g.col).to(dev)
+        else:
+            rowptr = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
+        broadcast_tensor_(rowptr, ctx, root)
+        if nnz:
+            broadcast_tensor_(col, ctx, root)
+        return rowptr, col, m
+    rowptr = broadcast_array(g.rowptr if ctx.rank == root else None, ctx, np.int64, n + 1, root)
+    col = broadcast_array(g.col if ctx.rank == root else None, ctx, np.int32, nnz, root)
+    return Graph(n, rowptr, col, m=m)
+
+
+def _qbits(K: int) -> int:
+    b = 1
+    while (1 << b) <= K:
+        b += 1
+    return b
+
+
+def allreduce_max(x: float, ctx: DistContext) -> float:
+    import torch
+    import torch.distributed as dist
+    if not ctx.distributed:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_comm_device(ctx))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum_i64(a: np.ndarray, ctx: DistContext) -> np.ndarray:
+    import torch
+    import torch.distributed as dist
+    if not ctx.distributed:
+        return a
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)).to(_comm_device(ctx))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistContext,
+                  stream=None) -> Tuple[int, int]:
+    """Global (minK, minF) with the reference tie-break. (-1, -1) when K == 0 (main.cu:379-380).
+
+    One all-reduce(MIN) of an int64 key F << qbits | q; falls back to two all-reduces when F is
+    too large to share 63 bits with the query index.
+    """
+    import torch
+    import torch.distributed as dist
+
+    F_local = np.asarray(F_local, dtype=np.int64)
+    idx_local = np.asarray(idx_local, dtype=np.int64)
+    qb = _qbits(K)
+    NONE = np.iinfo(np.int64).max
+    maxF = int(F_local.max()) if len(F_local) else 0
+    maxF = int(allreduce_max(maxF, ctx)) if ctx.distributed else maxF
+    dev = _comm_device(ctx) if ctx.distributed else None
+
+    def allmin(v: int) -> int:
+        if not ctx.distributed:
+            return v
+        t = torch.tensor([v], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t.item())
+
+    if qb < 63 and (maxF >> (63 - qb)) == 0:
+        keys = (F_local << qb) | idx_local
+        key = allmin(int(keys.min()) if len(keys) else NONE)
+        if key == NONE:
+            return -1, -1
+        return int(key & ((1 << qb) - 1)), int(key >> qb)
+    mf = allmin(int(F_local.min()) if len(F_local) else NONE)
+    if mf == NONE:
+        return -1, -1
+    cand = idx_local[F_local == mf]
+    mk = allmin(int(cand.min()) if len(cand) else NONE)
+    return mk, mf
+
+
+def gather_F(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistContext) -> np.ndarray:
+    """Full F vector on every rank (replaces MPI_Gather + MPI_Gatherv, main.cu:340-365)."""
+    full = np.zeros(K, dtype=np.int64)
+    full[np.asarray(idx_local, dtype=np.int64)] = F_local
+    return allreduce_sum_i64(full, ctx)

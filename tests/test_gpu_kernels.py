@@ -1,0 +1,123 @@
+"""GPU numerics: every device algorithm against the CPU oracle (exact integer F and edges)."""
+import numpy as np
+import pytest
+
+from golden import CASES
+
+pytestmark = pytest.mark.gpu
+
+DEVICE_ALGOS = ["bitpar", "dist", "topdown", "sweep"]
+
+
+def _graphs(m):
+    gs = [
+        ("rmat10", m.Graph.rmat(10, 16, 3)),
+        ("rmat12", m.Graph.rmat(12, 8, 5)),
+        ("uniform", m.Graph.uniform(3000, 9000, 11)),
+        ("grid", m.Graph.grid(40, 60, 0.9, 5, 2)),
+        ("sparse", m.Graph.uniform(5000, 2500, 4)),  # many small components + isolated vertices
+    ]
+    return gs
+
+
+@pytest.mark.parametrize("algo", DEVICE_ALGOS)
+def test_golden_cases(msbfs_pkg, algo):
+    m = msbfs_pkg
+    for (n, edges), groups, F, k, minf in CASES:
+        u = np.array([e[0] for e in edges], np.int32)
+        v = np.array([e[1] for e in edges], np.int32)
+        g = m.Graph.from_edges(n, u, v)
+        qs = m.QuerySet.from_groups(groups)
+        r = m.multi_source_bfs(g, qs, algo=algo)
+        assert list(r.F) == F
+        kk = m.argmin_first(r.F)
+        assert kk + 1 == k and (r.F[kk] if kk >= 0 else -1) == minf
+
+
+@pytest.mark.parametrize("algo", DEVICE_ALGOS)
+def test_algos_match_cpu(msbfs_pkg, algo):
+    m = msbfs_pkg
+    for name, g in _graphs(m):
+        qs = m.QuerySet.random(g.n, 70 if algo == "bitpar" else 9, 3, seed=len(name))
+        ref = m.cpu_bfs(g, qs, count_edges=True)
+        with m.Solver(g.to_device(0), algo, max_groups=qs.K) as s:
+            r = s.run(qs, count_edges=True)
+        assert np.array_equal(r.F, ref.F), (name, algo)
+        assert np.array_equal(r.edges, ref.edges), (name, algo)
+
+
+@pytest.mark.parametrize("K", [1, 63, 64, 65, 130, 300, 700, 1024, 1500])
+def test_bitpar_batch_widths(msbfs_pkg, K):
+    m = msbfs_pkg
+    g = m.Graph.rmat(11, 16, 9)
+    qs = m.QuerySet.random(g.n, K, 2, seed=K)
+    ref = m.cpu_bfs(g, qs)
+    with m.Solver(g.to_device(0), "bitpar", max_groups=K) as s:
+        assert np.array_equal(s.run(qs).F, ref.F)
+
+
+@pytest.mark.parametrize("force_dir,wide", [(1, 64), (2, 64), (0, 4), (2, 1), (0, 100000)])
+def test_bitpar_direction_variants(msbfs_pkg, force_dir, wide):
+    m = msbfs_pkg
+    for name, g in _graphs(m)[:4]:
+        qs = m.QuerySet.random(g.n, 200, 5, seed=3)
+        ref = m.cpu_bfs(g, qs, count_edges=True)
+        with m.Solver(g.to_device(0), "bitpar", max_groups=qs.K, force_dir=force_dir,
+                      wide_degree=wide) as s:
+            r = s.run(qs, count_edges=True)
+        assert np.array_equal(r.F, ref.F), (name, force_dir, wide)
+        assert np.array_equal(r.edges, ref.edges)
+
+
+@pytest.mark.parametrize("force_dir,wide", [(1, 64), (2, 64), (2, 2), (0, 8)])
+def test_dist_direction_variants(msbfs_pkg, force_dir, wide):
+    m = msbfs_pkg
+    for name, g in _graphs(m)[:4]:
+        qs = m.QuerySet.random(g.n, 6, 3, seed=5)
+        ref = m.cpu_bfs(g, qs)
+        with m.Solver(g.to_device(0), "dist", force_dir=force_dir, wide_degree=wide) as s:
+            assert np.array_equal(s.run(qs).F, ref.F), (name, force_dir, wide)
+
+
+def test_solver_reuse_is_deterministic(msbfs_pkg):
+    m = msbfs_pkg
+    g = m.DeviceGraph.rmat(13, 16, 2, device=0)
+    qs = m.QuerySet.random(g.n, 256, 8, seed=1)
+    with m.Solver(g, "bitpar", max_groups=qs.K) as s:
+        a = s.run(qs).F
+        b = s.run(qs).F
+        c = s.run(qs.subset(range(100))).F
+    assert np.array_equal(a, b) and np.array_equal(a[:100], c)
+
+
+def test_device_rmat_matches_host_generator(msbfs_pkg):
+    m = msbfs_pkg
+    dg = m.DeviceGraph.rmat(12, 16, 42, device=0)
+    hg = m.Graph.rmat(12, 16, 42)
+    d = dg.download()
+    assert d.n == hg.n and d.nnz == hg.nnz
+    assert np.array_equal(d.rowptr, hg.rowptr)
+    for v in range(0, hg.n, 7):
+        a = np.sort(d.col[d.rowptr[v]:d.rowptr[v + 1]])
+        b = np.sort(hg.col[hg.rowptr[v]:hg.rowptr[v + 1]])
+        assert np.array_equal(a, b)
+    dg.sort_rows()
+    s = dg.download()
+    for v in range(hg.n):
+        assert np.all(np.diff(s.col[s.rowptr[v]:s.rowptr[v + 1]]) >= 0)
+    assert dg.max_degree == int(np.diff(hg.rowptr).max())
+    assert dg.isolated == int((np.diff(hg.rowptr) == 0).sum())
+
+
+def test_device_uniform_and_wrap(msbfs_pkg):
+    import torch
+    m = msbfs_pkg
+    hg = m.Graph.uniform(4000, 20000, 3)
+    dg = m.DeviceGraph.uniform(4000, 20000, 3, device=0)
+    assert np.array_equal(dg.download().rowptr, hg.rowptr)
+    rp = torch.from_numpy(hg.rowptr).cuda()
+    cl = torch.from_numpy(hg.col).cuda()
+    wg = m.DeviceGraph.wrap(hg.n, rp, cl, device=0)
+    qs = m.QuerySet.random(hg.n, 50, 4, 1)
+    with m.Solver(wg, "bitpar", max_groups=50) as s:
+        assert np.array_equal(s.run(qs).F, m.cpu_bfs(hg, qs).F)

@@ -1,0 +1,25 @@
+#!/bin/bash
+# GPU-box session runner: each step has its own time limit; stop at the first fault/abort/timeout
+# (exit status > 1); plain test failures (status 1) are recorded and the session continues.
+set -u
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+step() {
+  local name=$1 limit=$2; shift 2
+  echo "== $name (limit ${limit}s): $*"
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -gt 1 ]; then echo "stopping: $name exited $rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) step smoke 300 python __graft_entry__.py smoke ;;
+    bench20) step bench20 300 python bench.py --scale 20 --steps 3 --warmup 1 --verify 32 ;;
+    bench22) step bench22 300 python bench.py --scale 22 --steps 3 --warmup 1 --verify 16 ;;
+    bench26) step bench26 900 python bench.py --steps 3 --warmup 1 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
