@@ -118,10 +118,11 @@ std::unique_ptr<Solver> make_dist_solver(const DeviceGraph& g);
 std::unique_ptr<Solver> make_sweep_solver(const DeviceGraph& g);
 
 // ---- common level-loop helpers (kernels/lbs.hip) ---------------------------------------------
-// Inclusive prefix sum of the degrees of `list[0..cnt)` into offs[0..cnt) (int64).
+// Inclusive prefix sum of ceil(degree / chunk) over `list[0..cnt)` into offs[0..cnt) (int64);
+// chunk = 1 gives the frontier's edge prefix used by the load-balanced top-down expansions.
 size_t frontier_scan_temp_bytes(int64_t max_items);
 void frontier_degree_scan(const int64_t* rowptr, const int32_t* list, int64_t cnt, int64_t* offs,
-                          void* temp, size_t temp_bytes, hipStream_t s);
+                          void* temp, size_t temp_bytes, hipStream_t s, int64_t chunk = 1);
 
 inline int grid_for(int64_t items, int per_block, int cap = 2048) {
   int64_t g = (items + per_block - 1) / per_block;

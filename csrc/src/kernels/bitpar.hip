@@ -15,16 +15,25 @@
 //    words and stops as soon as every still-alive group is covered (early exit). Double-buffered
 //    visited arrays make the pull race-free without a separate frontier array (a neighbour bit
 //    visited at any level <= L can only have been set exactly at L if it is still missing here).
+//    Low-degree vertices get G lanes each; high-degree vertices are cut into fixed-size edge
+//    chunks that many waves scan in parallel (partial ORs merged with atomicOr, then a finalize
+//    pass), so a 10^6-neighbour hub never serialises a level on one wave.
 //  * per-group F(U) = sum_level level * |newly visited| is accumulated on chip: every new bit adds
-//    `level` to a per-group LDS counter; one global atomic per group per block at the end. Only
-//    8 bytes per group ever leave the device (vs 4n bytes per query in the reference).
+//    to a per-group LDS counter; one global atomic per group per block at the end. Only 8 bytes
+//    per group ever leave the device (vs 4n bytes per query in the reference).
 //  * groups whose frontier died are masked out ("alive" words), so groups stuck in small
 //    components never stop other groups' vertices from finishing.
+//  * list building (active lists, frontiers, touched sets) goes through per-block LDS queues:
+//    one global atomic per ~1K items instead of one per wave (same-line atomics serialise).
 // Lane mapping for wave64: each lane owns VW (1-2) words = one 8-16 B load, a vertex's W words are
 // spread over G = W/VW consecutive lanes, so W=16 reads a vertex's 128-B line in one coalesced
 // wave-instruction slice.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "msbfs/device.hpp"
 
@@ -32,12 +41,16 @@ namespace msbfs {
 namespace bp {
 
 constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kQCap = 1024;       // LDS queue capacity (items) per block
+constexpr int kChunk = 1024;      // bottom-up edge chunk for wide vertices
 
 template <int W>
 struct Lay {
   static constexpr int VW = W >= 2 ? 2 : 1;
   static constexpr int G = W / VW;      // lanes per vertex
   static constexpr int VPW = 64 / G;    // vertices per wave
+  static constexpr int TILE = kWaves * VPW;  // vertices per block iteration
   static constexpr uint64_t GBITS = (G == 64) ? ~0ull : ((1ull << G) - 1);
 };
 
@@ -79,12 +92,24 @@ __device__ __forceinline__ V<VW> vzero() {
   return r;
 }
 
+// Device counters; every field on its own 128-B line so unrelated atomics never share a line.
+struct alignas(128) Slot32 {
+  uint32_t v;
+  uint32_t pad[31];
+};
+struct alignas(128) Slot64 {
+  unsigned long long v;
+  uint32_t pad[30];
+};
 struct Ctr {
+  Slot32 act2, actw2, fl2, touched;
+  Slot64 ef2;  // sum of degrees of the next frontier
+  Slot64 eu2;  // sum of degrees of the next active lists
+};
+// host view of the interesting fields
+struct HostCtr {
   uint32_t act2, actw2, fl2, touched;
-  unsigned long long ef2;  // sum of degrees of the next frontier
-  unsigned long long eu2;  // sum of degrees of the next active lists
-  uint32_t newcnt;          // vertices with new bits (== fl2)
-  uint32_t pad[3];
+  unsigned long long ef2, eu2;
 };
 
 __device__ __forceinline__ bool is_done(const uint32_t* done, int32_t v) {
@@ -94,13 +119,61 @@ __device__ __forceinline__ void set_done(uint32_t* done, int32_t v) {
   atomicOr(&done[v >> 5], 1u << (v & 31));
 }
 
-// sum a per-lane value over the wave and add it once to *dst (must be called converged)
-__device__ __forceinline__ void wave_sum_add(unsigned long long val, unsigned long long* dst) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
-  if (lane_id() == 0 && val) atomicAdd(dst, val);
+// ---- per-block LDS queues ---------------------------------------------------------------------
+struct LdsQueue {
+  int32_t item[kQCap];
+  uint32_t n;
+  uint32_t base;
+};
+
+__device__ __forceinline__ void q_init(LdsQueue& q) {
+  if (threadIdx.x == 0) q.n = 0;
 }
 
+// wave-aggregated push into the block queue (call from converged wave code)
+__device__ __forceinline__ void q_push(LdsQueue& q, bool pred, int32_t v) {
+  const uint64_t mask = __ballot(pred);
+  if (!mask) return;
+  const int leader = __ffsll((unsigned long long)mask) - 1;
+  uint32_t pos = 0;
+  if (lane_id() == leader) pos = atomicAdd(&q.n, (uint32_t)__popcll(mask));
+  pos = __shfl(pos, leader) + (uint32_t)__popcll(mask & lanemask_lt());
+  if (pred) q.item[pos] = v;
+}
+
+// Flush the queue to out[] when it may not hold another `room` items (or always, at the end).
+// Must be called by every thread of the block (block-uniform control flow).
+__device__ __forceinline__ void q_flush(LdsQueue& q, int32_t* out, uint32_t* gcnt, int room,
+                                        bool force) {
+  __syncthreads();
+  const uint32_t n = q.n;
+  __syncthreads();
+  if (n == 0 || (!force && n + (uint32_t)room <= (uint32_t)kQCap)) return;
+  if (threadIdx.x == 0) q.base = atomicAdd(gcnt, n);
+  __syncthreads();
+  const uint32_t base = q.base;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[base + i] = q.item[i];
+  __syncthreads();
+  if (threadIdx.x == 0) q.n = 0;
+  __syncthreads();
+}
+
+// block-wide sum of per-thread values, one atomic per block
+__device__ __forceinline__ void block_sum_add(unsigned long long val, unsigned long long* dst,
+                                              unsigned long long* scratch /*kWaves*/) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
+  __syncthreads();
+  if (lane_id() == 0) scratch[threadIdx.x >> 6] = val;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kWaves; ++w) t += scratch[w];
+    if (t) atomicAdd(dst, t);
+  }
+}
+
+// ---- per-group level counters in LDS ------------------------------------------------------------
 template <int W, bool COUNT>
 struct Lds {
   uint32_t f[64 * W];
@@ -113,7 +186,6 @@ __device__ __forceinline__ void lds_zero(Lds<W, COUNT>& s) {
     s.f[i] = 0;
     if constexpr (COUNT) s.e[i] = 0;
   }
-  __syncthreads();
 }
 
 template <int W, bool COUNT>
@@ -160,12 +232,15 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_
                                                  uint64_t* visB, uint64_t* acc, int32_t* stamp,
                                                  int32_t epoch, int32_t* fl, Ctr* ctr,
                                                  unsigned long long* E, uint64_t* alive) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t lim = (np + stride - 1) / stride * stride;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
+  __shared__ LdsQueue q;
+  __shared__ unsigned long long scratch[kWaves];
+  q_init(q);
+  __syncthreads();
+  unsigned long long ef = 0;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < np; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = b + threadIdx.x;
     bool app = false;
     int32_t v = 0;
-    unsigned long long deg = 0;
     if (i < np) {
       v = pv[i];
       const int k = pk[i];
@@ -176,15 +251,17 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_
         atomicOr((unsigned long long*)&visB[(int64_t)v * W + word], bit);
         atomicOr((unsigned long long*)&acc[(int64_t)v * W + word], bit);
         atomicOr((unsigned long long*)&alive[word], bit);
-        deg = (unsigned long long)(rowptr[v + 1] - rowptr[v]);
+        const unsigned long long deg = (unsigned long long)(rowptr[v + 1] - rowptr[v]);
         if constexpr (COUNT) atomicAdd(&E[k], deg);
         app = atomicExch(&stamp[v], epoch) != epoch;
+        if (app) ef += deg;
       }
     }
-    const uint32_t pos = wave_append(app, &ctr->fl2);
-    if (app) fl[pos] = v;
-    wave_sum_add(app ? deg : 0ull, &ctr->ef2);
+    q_push(q, app, v);
+    q_flush(q, fl, &ctr->fl2.v, kBlock, false);
   }
+  q_flush(q, fl, &ctr->fl2.v, 0, true);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -198,13 +275,15 @@ __global__ __launch_bounds__(kBlock) void k_td_expand(
     const uint64_t* visCur, const uint64_t* fsrc, const uint32_t* done, uint64_t* accNext,
     int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr) {
   using L = Lay<W>;
-  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  __shared__ LdsQueue q;
+  q_init(q);
+  __syncthreads();
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
   const int64_t total = offs[nf - 1];
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t eb = wave * VPW; eb < total; eb += nwaves * VPW) {
-    const int64_t e = eb + sub;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < total; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t e = tb + wv * VPW + sub;
     bool touch = false;
     int32_t v = 0;
     if (e < total) {
@@ -232,14 +311,15 @@ __global__ __launch_bounds__(kBlock) void k_td_expand(
             any = true;
           }
         }
-        // one lane per group decides the first touch of v in this level
+        // one lane per group decides the first touch of v in this level (the group shares v)
         const uint64_t gm = (__ballot(any) >> (sub * G)) & L::GBITS;
         if (gm && slot == 0) touch = atomicExch(&stamp[v], epoch) != epoch;
       }
     }
-    const uint32_t pos = wave_append(touch, &ctr->touched);
-    if (touch) touched[pos] = v;
+    q_push(q, touch, v);
+    q_flush(q, touched, &ctr->touched.v, TILE, false);
   }
+  q_flush(q, touched, &ctr->touched.v, 0, true);
 }
 
 // top-down finalize: new = acc & ~vis; update both visited buffers; build the next frontier.
@@ -250,21 +330,25 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
     Ctr* ctr, unsigned long long* F, unsigned long long* E, uint64_t* alive_next, uint32_t level,
     const int32_t* fl_old, int64_t nf_old, uint64_t* accCur_zero) {
   using L = Lay<W>;
-  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ Lds<W, COUNT> s;
+  __shared__ LdsQueue q;
+  __shared__ unsigned long long scratch[kWaves];
   lds_zero(s);
-  const int64_t nt = ctr->touched;  // written by k_td_expand (previous kernel on the stream)
+  q_init(q);
+  __syncthreads();
+  const int64_t nt = ctr->touched.v;  // written by k_td_expand (previous kernel on the stream)
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int wv = threadIdx.x >> 6;
   V<VW> am, gm;
 #pragma unroll
   for (int j = 0; j < VW; ++j) {
     am.w[j] = alive[slot * VW + j];
     gm.w[j] = gmask[slot * VW + j];
   }
-  for (int64_t b = wave * VPW; b < nt; b += nwaves * VPW) {
-    const int64_t idx = b + sub;
+  unsigned long long ef = 0;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nt; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t idx = tb + wv * VPW + sub;
     const bool valid = idx < nt;
     int32_t v = 0;
     bool anynew = false, notfull = false;
@@ -294,13 +378,17 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
     const bool leader = valid && slot == 0;
     if (leader && g_full) set_done(done, v);
     const bool app = leader && g_new;
-    const uint32_t pos = wave_append(app, &ctr->fl2);
-    if (app) fl2[pos] = v;
-    wave_sum_add(app ? (unsigned long long)deg : 0ull, &ctr->ef2);
+    if (app) ef += deg;
     if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
+    q_push(q, app, v);
+    q_flush(q, fl2, &ctr->fl2.v, TILE, false);
   }
+  q_flush(q, fl2, &ctr->fl2.v, 0, true);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
   // zero the consumed top-down frontier bits of the previous frontier
   if (accCur_zero) {
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t b = wave * VPW; b < nf_old; b += nwaves * VPW) {
       const int64_t idx = b + sub;
       if (idx < nf_old) stv<VW>(accCur_zero + (int64_t)fl_old[idx] * W + slot * VW, vzero<VW>());
@@ -326,46 +414,58 @@ __global__ __launch_bounds__(kBlock) void k_zero_acc(const int32_t* fl, int64_t 
 __global__ __launch_bounds__(kBlock) void k_build_active(int64_t n, const int64_t* rowptr,
                                                          const uint32_t* done, int wide_deg,
                                                          int32_t* act, int32_t* actw, Ctr* ctr) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t lim = (n + stride - 1) / stride * stride;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
+  __shared__ LdsQueue qn, qw;
+  __shared__ unsigned long long scratch[kWaves];
+  q_init(qn);
+  q_init(qw);
+  __syncthreads();
+  unsigned long long eu = 0;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < n; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = b + threadIdx.x;
     int64_t d = 0;
     bool ok = false;
     if (i < n) {
       d = rowptr[i + 1] - rowptr[i];
       ok = d > 0 && !is_done(done, (int32_t)i);
     }
-    const bool w = ok && d > wide_deg, nrw = ok && d <= wide_deg;
-    const uint32_t p1 = wave_append(nrw, &ctr->act2);
-    const uint32_t p2 = wave_append(w, &ctr->actw2);
-    if (nrw) act[p1] = (int32_t)i;
-    if (w) actw[p2] = (int32_t)i;
-    wave_sum_add(ok ? (unsigned long long)d : 0ull, &ctr->eu2);
+    if (ok) eu += (unsigned long long)d;
+    q_push(qn, ok && d <= wide_deg, (int32_t)i);
+    q_push(qw, ok && d > wide_deg, (int32_t)i);
+    q_flush(qn, act, &ctr->act2.v, kBlock, false);
+    q_flush(qw, actw, &ctr->actw2.v, kBlock, false);
   }
+  q_flush(qn, act, &ctr->act2.v, 0, true);
+  q_flush(qw, actw, &ctr->actw2.v, 0, true);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
 }
 
 // ---------------------------------------------------------------------------------------------
-// bottom-up, narrow vertices: G lanes per vertex, 4 neighbours in flight per lane, early exit
+// bottom-up, narrow vertices: G lanes per vertex, U neighbours in flight per lane, early exit
 // when every alive group is covered.
 // ---------------------------------------------------------------------------------------------
-template <int W, bool COUNT>
+template <int W, bool COUNT, int U>
 __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, unsigned long long* F, unsigned long long* E,
     uint64_t* alive_next, uint32_t level) {
   using L = Lay<W>;
-  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ Lds<W, COUNT> s;
+  __shared__ LdsQueue qa, qf;
+  __shared__ unsigned long long scratch[kWaves];
   lds_zero(s);
+  q_init(qa);
+  q_init(qf);
+  __syncthreads();
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int wv = threadIdx.x >> 6;
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  for (int64_t b = wave * VPW; b < nact; b += nwaves * VPW) {
-    const int64_t idx = b + sub;
+  unsigned long long eu = 0, ef = 0;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nact; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t idx = tb + wv * VPW + sub;
     const bool valid = idx < nact;
     int32_t v = 0;
     V<VW> r = vzero<VW>(), unv = vzero<VW>(), acc = vzero<VW>();
@@ -386,20 +486,21 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     if (g_open) {
       int64_t e = beg;
       while (e < end) {
-        int32_t u[4];
+        int32_t u[U];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) u[q] = (e + q < end) ? col[e + q] : -1;
-        V<VW> x[4];
+        for (int q = 0; q < U; ++q) u[q] = (e + q < end) ? col[e + q] : -1;
+        V<VW> x[U];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < U; ++q)
           x[q] = u[q] >= 0 ? ldv<VW>(R + (int64_t)u[q] * W + slot * VW) : vzero<VW>();
         bool cov = true;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
-          acc.w[j] |= (x[0].w[j] | x[1].w[j] | x[2].w[j] | x[3].w[j]);
+#pragma unroll
+          for (int q = 0; q < U; ++q) acc.w[j] |= x[q].w[j];
           cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
         }
-        e += 4;
+        e += U;
         // the whole group runs this loop in lock step (same v); exit when all lanes covered
         if (!((__ballot(!cov) >> (sub * G)) & L::GBITS)) break;
       }
@@ -424,105 +525,155 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     const bool leader = valid && slot == 0;
     const uint32_t deg = (uint32_t)(end - beg);
     if (leader && !g_nf) set_done(done, v);
-    const bool keep = leader && g_nf;
-    const uint32_t p1 = wave_append(keep, &ctr->act2);
-    if (keep) act2[p1] = v;
-    wave_sum_add(keep ? (unsigned long long)deg : 0ull, &ctr->eu2);
-    const bool app = leader && g_new;
-    const uint32_t p2 = wave_append(app, &ctr->fl2);
-    if (app) fl2[p2] = v;
-    wave_sum_add(app ? (unsigned long long)deg : 0ull, &ctr->ef2);
+    const bool keep = leader && g_nf, app = leader && g_new;
+    if (keep) eu += deg;
+    if (app) ef += deg;
     if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
+    q_push(qa, keep, v);
+    q_push(qf, app, v);
+    q_flush(qa, act2, &ctr->act2.v, TILE, false);
+    q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
   }
+  q_flush(qa, act2, &ctr->act2.v, 0, true);
+  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
   lds_flush<W, COUNT>(s, F, E, alive_next, level);
 }
 
-// bottom-up, wide vertices: one wave per vertex; S = 64/G sub-groups stride the neighbour list
-// and OR-reduce across sub-groups once per 4*S neighbours for the early-exit test.
-template <int W, bool COUNT>
-__global__ __launch_bounds__(kBlock) void k_bu_wide(
-    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
-    const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
-    int32_t* act2, int32_t* fl2, Ctr* ctr, unsigned long long* F, unsigned long long* E,
-    uint64_t* alive_next, uint32_t level) {
+// bottom-up, wide vertices, phase 1: one wave per edge chunk (<= kChunk edges). S = 64/G
+// sub-groups stride the chunk, OR-reduce across sub-groups for the early-exit test, and merge
+// the chunk's new bits into acc[v] with atomicOr. offs = inclusive prefix of chunk counts.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_bu_chunks(
+    const int32_t* wl, int64_t nw, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, const uint64_t* alive, const uint64_t* gmask, uint64_t* acc) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
-  __shared__ Lds<W, COUNT> s;
-  lds_zero(s);
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int64_t nchunks = offs[nw - 1];
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  for (int64_t idx = wave; idx < nact; idx += nwaves) {
-    const int32_t v = act[idx];
-    const V<VW> r = ldv<VW>(R + (int64_t)v * W + slot * VW);
-    V<VW> unv, acc = vzero<VW>();
+  for (int64_t c = wave; c < nchunks; c += nwaves) {
+    const int64_t i = upper_bound_i64(offs, nw, c);
+    const int32_t v = wl[i];
+    const int64_t j0 = c - (i ? offs[i - 1] : 0);
+    const int64_t end = rowptr[v + 1];
+    const int64_t beg = rowptr[v] + j0 * kChunk;
+    const int64_t lim = min(end, beg + (int64_t)kChunk);
+    const int64_t vo = (int64_t)v * W + slot * VW;
+    const V<VW> r = ldv<VW>(R + vo);
+    // snapshot of bits other chunks already found (a hint; stale values only cost work)
+    const V<VW> g = ldv<VW>(acc + vo);
+    V<VW> unv, a = vzero<VW>();
     bool lane_open = false;
 #pragma unroll
     for (int j = 0; j < VW; ++j) {
       unv.w[j] = ~r.w[j] & am.w[j];
-      lane_open |= unv.w[j] != 0;
+      lane_open |= (unv.w[j] & ~g.w[j]) != 0;
     }
-    const bool open = __ballot(lane_open) != 0;
-    const int64_t beg = rowptr[v], end = rowptr[v + 1];
-    if (open) {
-      for (int64_t e0 = beg; e0 < end; e0 += 4 * S) {
-        int32_t u[4];
+    if (!__ballot(lane_open)) continue;  // wave-uniform
+    for (int64_t e0 = beg; e0 < lim; e0 += 4 * S) {
+      int32_t u[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int64_t e = e0 + sub + (int64_t)q * S;
-          u[q] = e < end ? col[e] : -1;
+      for (int q = 0; q < 4; ++q) {
+        const int64_t e = e0 + sub + (int64_t)q * S;
+        u[q] = e < lim ? col[e] : -1;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (u[q] >= 0) {
+          const V<VW> x = ldv<VW>(R + (int64_t)u[q] * W + slot * VW);
+#pragma unroll
+          for (int j = 0; j < VW; ++j) a.w[j] |= x.w[j];
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (u[q] >= 0) {
-            const V<VW> x = ldv<VW>(R + (int64_t)u[q] * W + slot * VW);
+      for (int off = G; off < 64; off <<= 1)
 #pragma unroll
-            for (int j = 0; j < VW; ++j) acc.w[j] |= x.w[j];
-          }
-        // OR-reduce across sub-groups (lane bits >= log2 G)
+        for (int j = 0; j < VW; ++j) a.w[j] |= __shfl_xor(a.w[j], off);
+      bool cov = true;
 #pragma unroll
-        for (int off = G; off < 64; off <<= 1)
+      for (int j = 0; j < VW; ++j) cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
+      if (!__ballot(!cov)) break;
+    }
+    if (sub == 0) {
 #pragma unroll
-          for (int j = 0; j < VW; ++j) acc.w[j] |= __shfl_xor(acc.w[j], off);
-        bool cov = true;
-#pragma unroll
-        for (int j = 0; j < VW; ++j) cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
-        if (!__ballot(!cov)) break;
+      for (int j = 0; j < VW; ++j) {
+        const uint64_t nb = a.w[j] & unv.w[j] & ~g.w[j];
+        if (nb) atomicOr((unsigned long long*)&acc[vo + j], nb);
       }
     }
-    V<VW> nw;
-    bool anynew = false, notfull = false;
+  }
+}
+
+// bottom-up, wide vertices, phase 2: G lanes per vertex fold acc[v] into the visited words.
+template <int W, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
+    const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, uint64_t* Wb,
+    uint64_t* acc, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* actw2,
+    int32_t* fl2, Ctr* ctr, unsigned long long* F, unsigned long long* E, uint64_t* alive_next,
+    uint32_t level) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  __shared__ Lds<W, COUNT> s;
+  __shared__ LdsQueue qa, qf;
+  __shared__ unsigned long long scratch[kWaves];
+  lds_zero(s);
+  q_init(qa);
+  q_init(qf);
+  __syncthreads();
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  V<VW> am;
 #pragma unroll
-    for (int j = 0; j < VW; ++j) {
-      nw.w[j] = acc.w[j] & unv.w[j];
-      anynew |= nw.w[j] != 0;
-      notfull |= (unv.w[j] & ~nw.w[j]) != 0;
-    }
-    if (open && sub == 0) {
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  unsigned long long eu = 0, ef = 0;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nw; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t idx = tb + wv * VPW + sub;
+    const bool valid = idx < nw;
+    int32_t v = 0;
+    V<VW> nwb = vzero<VW>();
+    bool anynew = false, notfull = false;
+    uint32_t deg = 0;
+    if (valid) {
+      v = wl[idx];
+      const int64_t vo = (int64_t)v * W + slot * VW;
+      const V<VW> r = ldv<VW>(R + vo);
+      const V<VW> a = ldv<VW>(acc + vo);
       V<VW> nv;
 #pragma unroll
-      for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
-      stv<VW>(Wb + (int64_t)v * W + slot * VW, nv);
-    }
-    const bool g_new = __ballot(anynew) != 0;
-    const bool g_nf = __ballot(notfull) != 0;
-    const uint32_t deg = (uint32_t)(end - beg);
-    if (lane == 0) {
-      if (!g_nf) set_done(done, v);
-      else {
-        act2[atomicAdd(&ctr->actw2, 1u)] = v;
-        atomicAdd(&ctr->eu2, (unsigned long long)deg);
+      for (int j = 0; j < VW; ++j) {
+        const uint64_t unv = ~r.w[j] & am.w[j];
+        nwb.w[j] = a.w[j] & unv;
+        nv.w[j] = r.w[j] | nwb.w[j];
+        anynew |= nwb.w[j] != 0;
+        notfull |= (unv & ~nwb.w[j]) != 0;
       }
-      if (g_new) {
-        fl2[atomicAdd(&ctr->fl2, 1u)] = v;
-        atomicAdd(&ctr->ef2, (unsigned long long)deg);
-      }
+      stv<VW>(acc + vo, vzero<VW>());
+      stv<VW>(Wb + vo, nv);
+      deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
     }
-    if (anynew && sub == 0) count_bits<W, COUNT>(s, nw, slot, deg);
+    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
+    const bool g_new = (bn >> (sub * G)) & L::GBITS;
+    const bool g_nf = (bf >> (sub * G)) & L::GBITS;
+    const bool leader = valid && slot == 0;
+    if (leader && !g_nf) set_done(done, v);
+    const bool keep = leader && g_nf, app = leader && g_new;
+    if (keep) eu += deg;
+    if (app) ef += deg;
+    if (anynew) count_bits<W, COUNT>(s, nwb, slot, deg);
+    q_push(qa, keep, v);
+    q_push(qf, app, v);
+    q_flush(qa, actw2, &ctr->actw2.v, TILE, false);
+    q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
   }
+  q_flush(qa, actw2, &ctr->actw2.v, 0, true);
+  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
   lds_flush<W, COUNT>(s, F, E, alive_next, level);
 }
 
@@ -557,6 +708,8 @@ class BitparSolver final : public Solver {
     ctr_.alloc(sizeof(Ctr));
     small_.alloc(64 * 16 * sizeof(unsigned long long) * 2 + 4 * 16 * sizeof(uint64_t));
     hctr_ = std::make_unique<PinnedBuf>(sizeof(Ctr));
+    if (const char* d = getenv("MSBFS_DIRS")) dirs_ = d;  // per-level T/B override (tuning)
+    if (const char* u = getenv("MSBFS_UNROLL")) unroll_ = atoi(u);
     MSBFS_HIP_CHECK(hipDeviceSynchronize());
   }
 
@@ -598,12 +751,11 @@ class BitparSolver final : public Solver {
 #undef MSBFS_BP_CASE
   }
 
-  Ctr read_ctr(hipStream_t s) {
+  HostCtr read_ctr(hipStream_t s) {
     MSBFS_HIP_CHECK(hipMemcpyAsync(hctr_->p, ctr_.p, sizeof(Ctr), hipMemcpyDeviceToHost, s));
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
-    Ctr c;
-    std::memcpy(&c, hctr_->p, sizeof(Ctr));
-    return c;
+    const Ctr* c = hctr_->as<Ctr>();
+    return HostCtr{c->act2.v, c->actw2.v, c->fl2.v, c->touched.v, c->ef2.v, c->eu2.v};
   }
 
   const DeviceGraph& g_;
@@ -613,11 +765,14 @@ class BitparSolver final : public Solver {
   size_t scan_bytes_ = 0;
   std::unique_ptr<PinnedBuf> hctr_;
   int32_t epoch_ = 0;
+  std::string dirs_;
+  int unroll_ = 4;
 };
 
 template <int W, bool COUNT>
 void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
                               int64_t* Fout, int64_t* edges2, RunStats* st, hipStream_t s) {
+  using L = Lay<W>;
   const int64_t n = g_.n;
   const size_t vb = (size_t)std::max<int64_t>(n, 1) * W * sizeof(uint64_t);
   // ---- per-batch state reset
@@ -636,9 +791,8 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
     MSBFS_HIP_CHECK(hipMemcpyAsync(gmask, hm, sizeof(hm), hipMemcpyHostToDevice, s));
   }
   // ---- sources: (vertex, local group) pairs, out-of-range ids dropped (main.cu:49)
-  std::vector<int32_t> hp;
+  std::vector<int32_t> hp, hk;
   hp.reserve(2 * (qoff[k0 + nb] - qoff[k0]));
-  std::vector<int32_t> hk;
   for (int64_t k = 0; k < nb; ++k)
     for (int64_t j = qoff[k0 + k]; j < qoff[k0 + k + 1]; ++j) {
       const int32_t v = qids[j];
@@ -668,7 +822,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
         ctr_.as<Ctr>(), dE, alive[0]);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
-  Ctr c = read_ctr(s);
+  HostCtr c = read_ctr(s);
   int64_t nf = c.fl2, ef = (int64_t)c.ef2;
   int64_t na = n, ea = g_.nnz;  // active estimate before the first bottom-up build
   int64_t nact = 0, nactw = 0;
@@ -676,12 +830,16 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
   int alv = 0;
   uint32_t level = 0;
   const int grid = 2048;
+  static const bool trace = getenv("MSBFS_TRACE") != nullptr;
+  auto tl = std::chrono::steady_clock::now();
   while (nf > 0) {
     // direction choice (Beamer et al. SC'12, on the union frontier)
     if (opt.force_dir == 1) bottom_up = false;
     else if (opt.force_dir == 2) bottom_up = level > 0;
     else if (!bottom_up) bottom_up = (double)ef > (double)ea / opt.alpha;
     else bottom_up = !((double)nf < (double)na / opt.beta && (double)ef < (double)ea / opt.alpha);
+    if (level < dirs_.size() && (dirs_[level] == 'T' || dirs_[level] == 'B'))
+      bottom_up = dirs_[level] == 'B';
     MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
     MSBFS_HIP_CHECK(hipMemsetAsync(alive[alv ^ 1], 0, 16 * sizeof(uint64_t), s));
     ++level;
@@ -692,8 +850,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
       frontier_degree_scan(g_.rowptr, fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(),
                            scan_tmp_.p, scan_bytes_, s);
       ++epoch_;
-      const int64_t groups = (ef + Lay<W>::VPW - 1) / Lay<W>::VPW;
-      const int eg = grid_for(groups, kBlock / 64, 8192);
+      const int eg = grid_for(ef, L::TILE, 8192);
       if (fsrc_acc)
         k_td_expand<W, false><<<eg, kBlock, 0, s>>>(
             fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
@@ -707,7 +864,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
       MSBFS_HIP_CHECK(hipGetLastError());
       // touched <= min(n, frontier edges); the kernel reads the exact count from ctr
       const int64_t nt_max = std::min<int64_t>(std::max<int64_t>(ef, nf), n);
-      k_td_finalize<W, COUNT><<<grid_for(nt_max, kBlock / 64 * Lay<W>::VPW, grid), kBlock, 0, s>>>(
+      k_td_finalize<W, COUNT><<<grid_for(nt_max, L::TILE, grid), kBlock, 0, s>>>(
           touched_.as<int32_t>(), g_.rowptr, R, O, acc_[ac ^ 1].as<uint64_t>(), alive[alv],
           gmask, done_.as<uint32_t>(), fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), dF, dE,
           alive[alv ^ 1], level, fl_[fc].as<int32_t>(), nf,
@@ -719,7 +876,6 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
     } else {
       // ---- bottom-up
       if (!have_active) {
-        MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
         k_build_active<<<grid_for(n, kBlock), kBlock, 0, s>>>(
             n, g_.rowptr, done_.as<uint32_t>(), opt.wide_degree, act_[0].as<int32_t>(),
             actw_[0].as<int32_t>(), ctr_.as<Ctr>());
@@ -731,22 +887,34 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
         MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
       }
       if (fsrc_acc) {
-        // bottom-up does not read frontier bits; clear the pending top-down ones
-        k_zero_acc<W><<<grid_for(nf * Lay<W>::G, kBlock), kBlock, 0, s>>>(
+        // bottom-up does not read frontier bits; clear the pending top-down ones so acc_[ac]
+        // is all-zero and can collect the wide vertices' chunk results
+        k_zero_acc<W><<<grid_for(nf * L::G, kBlock), kBlock, 0, s>>>(
             fl_[fc].as<int32_t>(), nf, acc_[ac].as<uint64_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
       }
-      if (nact)
-        k_bu_narrow<W, COUNT><<<grid_for(nact, kBlock / 64 * Lay<W>::VPW, grid), kBlock, 0, s>>>(
+      if (nact) {
+        auto kern = unroll_ >= 8 ? k_bu_narrow<W, COUNT, 8> : k_bu_narrow<W, COUNT, 4>;
+        kern<<<grid_for(nact, L::TILE, grid), kBlock, 0, s>>>(
             act_[0].as<int32_t>(), nact, g_.rowptr, g_.col, R, O, alive[alv], gmask,
             done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
             ctr_.as<Ctr>(), dF, dE, alive[alv ^ 1], level);
-      if (nactw)
-        k_bu_wide<W, COUNT><<<grid_for(nactw, kBlock / 64, grid), kBlock, 0, s>>>(
-            actw_[0].as<int32_t>(), nactw, g_.rowptr, g_.col, R, O, alive[alv], gmask,
-            done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
+        MSBFS_HIP_CHECK(hipGetLastError());
+      }
+      if (nactw) {
+        frontier_degree_scan(g_.rowptr, actw_[0].as<int32_t>(), nactw, offs_.as<int64_t>(),
+                             scan_tmp_.p, scan_bytes_, s, kChunk);
+        const int64_t chunks_max = nactw + ea / kChunk + 1;
+        k_bu_chunks<W><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
+            actw_[0].as<int32_t>(), nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
+            alive[alv], gmask, acc_[ac].as<uint64_t>());
+        MSBFS_HIP_CHECK(hipGetLastError());
+        k_bu_wide_finalize<W, COUNT><<<grid_for(nactw, L::TILE, grid), kBlock, 0, s>>>(
+            actw_[0].as<int32_t>(), nactw, g_.rowptr, R, O, acc_[ac].as<uint64_t>(), alive[alv],
+            gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
             ctr_.as<Ctr>(), dF, dE, alive[alv ^ 1], level);
-      MSBFS_HIP_CHECK(hipGetLastError());
+        MSBFS_HIP_CHECK(hipGetLastError());
+      }
       std::swap(act_[0], act_[1]);
       std::swap(actw_[0], actw_[1]);
       cur ^= 1;
@@ -759,6 +927,16 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
       nactw = c.actw2;
       na = nact + nactw;
       ea = (int64_t)c.eu2;
+    }
+    if (trace) {
+      const auto t2 = std::chrono::steady_clock::now();
+      fprintf(stderr,
+              "[msbfs bp W=%d] level %u %s nf=%lld ef=%lld -> nf'=%lld ef'=%lld touched=%u "
+              "active=%lld (wide %lld) ea=%lld  %.3f ms\n",
+              W, level, bottom_up ? "BU" : "TD", (long long)nf, (long long)ef,
+              (long long)c.fl2, (long long)c.ef2, c.touched, (long long)na, (long long)nactw,
+              (long long)ea, std::chrono::duration<double, std::milli>(t2 - tl).count());
+      tl = t2;
     }
     nf = c.fl2;
     ef = (int64_t)c.ef2;

@@ -321,11 +321,12 @@ void device_graph_sort_rows(DeviceGraph& g, hipStream_t s) {
 // ---- frontier degree scan (shared by the level loops) ----------------------------------------
 namespace {
 __global__ __launch_bounds__(kBlock) void k_list_degrees(const int64_t* rowptr, const int32_t* list,
-                                                         int64_t cnt, int64_t* out) {
+                                                         int64_t cnt, int64_t* out, int64_t chunk) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += stride) {
     const int32_t v = list[i];
-    out[i] = rowptr[v + 1] - rowptr[v];
+    const int64_t d = rowptr[v + 1] - rowptr[v];
+    out[i] = chunk == 1 ? d : (d + chunk - 1) / chunk;
   }
 }
 }  // namespace
@@ -338,12 +339,12 @@ size_t frontier_scan_temp_bytes(int64_t max_items) {
 }
 
 void frontier_degree_scan(const int64_t* rowptr, const int32_t* list, int64_t cnt, int64_t* offs,
-                          void* temp, size_t temp_bytes, hipStream_t s) {
+                          void* temp, size_t temp_bytes, hipStream_t s, int64_t chunk) {
   if (cnt <= 0) return;
   int64_t* degs = (int64_t*)temp;
   char* t2 = (char*)temp + (((size_t)cnt * sizeof(int64_t) + 255) & ~size_t(255));
   size_t tb = temp_bytes - ((size_t)(t2 - (char*)temp));
-  k_list_degrees<<<grid_for(cnt, kBlock), kBlock, 0, s>>>(rowptr, list, cnt, degs);
+  k_list_degrees<<<grid_for(cnt, kBlock), kBlock, 0, s>>>(rowptr, list, cnt, degs, chunk);
   MSBFS_HIP_CHECK(hipGetLastError());
   MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(t2, tb, degs, offs, (int)cnt, s));
 }

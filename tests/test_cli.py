@@ -1,0 +1,110 @@
+"""The native CLI keeps the reference contract: flags, usage/exit code, 7-line report, errors,
+and identical answers for every MPI world size (round-robin invariance, main.cu:305)."""
+import os
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from golden import CASES
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MPIEXEC = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
+
+
+def _cli(msbfs):
+    p = msbfs.native.CLI_PATH
+    if not os.path.exists(p):
+        pytest.skip("native CLI not built")
+    return p
+
+
+def _write_case(tmp_path, m, case, idx):
+    (n, edges), groups = case[0], case[1]
+    g = m.Graph.from_edges(n, np.array([e[0] for e in edges], np.int32),
+                           np.array([e[1] for e in edges], np.int32))
+    gp, qp = str(tmp_path / f"g{idx}.bin"), str(tmp_path / f"q{idx}.bin")
+    g.write(gp)
+    m.QuerySet.from_groups(groups).write(qp)
+    return gp, qp
+
+
+def _run(cmd, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run(cmd, capture_output=True, text=True, env=e, timeout=300)
+
+
+@pytest.mark.parametrize("idx", range(len(CASES)))
+def test_cli_golden_report(tmp_path, msbfs_pkg, idx):
+    m = msbfs_pkg
+    gp, qp = _write_case(tmp_path, m, CASES[idx], idx)
+    r = _run([_cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo", "cpu", "--no-cache"],
+             {"MSBFS_NO_MPI": "1"})
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert len(lines) == 7
+    assert lines[0] == f"Graph: {gp}" and lines[1] == f"Query: {qp}"
+    assert lines[2] == f"Query number (k) with minimum F value: {CASES[idx][3]}"
+    assert lines[3] == f"Minimum F value: {CASES[idx][4]}"
+    assert lines[4] == "GPU # : 1 GPU"
+    assert lines[5].startswith("Preprocessing time: ") and lines[5].endswith(" s")
+    assert len(lines[5].split()[2].split(".")[1]) == 9  # fixed << setprecision(9)
+    assert lines[6].startswith("Computation time: ")
+
+
+def test_cli_usage_and_errors(tmp_path, msbfs_pkg):
+    cli = _cli(msbfs_pkg)
+    r = _run([cli, "-g", "x"], {"MSBFS_NO_MPI": "1"})
+    assert r.returncode == 255 and "Usage: mpirun -np <ranks>" in r.stderr
+    assert "-g <graph.bin> -q <query.bin> -gn <numGPU>" in r.stderr
+    r = _run([cli, "-g", str(tmp_path / "nope.bin"), "-q", "q", "-gn", "1", "--algo", "cpu"],
+             {"MSBFS_NO_MPI": "1"})
+    assert r.returncode != 0 and "Could not open graph file" in r.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+@pytest.mark.parametrize("ranks", [1, 2, 3, 5])
+def test_cli_mpi_world_size_invariance(tmp_path, msbfs_pkg, ranks):
+    m = msbfs_pkg
+    g = m.Graph.rmat(10, 8, 4)
+    gp, qp = str(tmp_path / "r.bin"), str(tmp_path / "q.bin")
+    g.write(gp)
+    qs = m.QuerySet.random(g.n, 4, 2, 3)  # K=4 < ranks=5 -> idle ranks (main.cu:305)
+    qs.write(qp)
+    ref = m.cpu_bfs(g, qs)
+    k = m.argmin_first(ref.F)
+    r = _run([MPIEXEC, "-n", str(ranks), _cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo", "cpu",
+              "--no-cache", "--json"])
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[2] == f"Query number (k) with minimum F value: {k + 1}"
+    assert lines[3] == f"Minimum F value: {ref.F[k]}"
+    import json
+    js = json.loads(lines[7])
+    assert js["F"] == list(map(int, ref.F)) and js["ranks"] == ranks and js["comm"] == "mpi"
+
+
+def test_cli_generator_mode(msbfs_pkg):
+    m = msbfs_pkg
+    r = _run([_cli(m), "--gen", "rmat:9:8:2", "--qgen", "20:3:5", "-gn", "1", "--algo", "cpu",
+              "--json"], {"MSBFS_NO_MPI": "1"})
+    assert r.returncode == 0, r.stderr
+    g = m.Graph.rmat(9, 8, 2)
+    ref = m.cpu_bfs(g, m.QuerySet.random(g.n, 20, 3, 5))
+    import json
+    assert json.loads(r.stdout.splitlines()[7])["F"] == list(map(int, ref.F))
+
+
+def test_python_cli_matches(tmp_path, msbfs_pkg):
+    m = msbfs_pkg
+    gp, qp = _write_case(tmp_path, m, CASES[1], 1)
+    r = _run([sys.executable, "-m", "msbfs", "-g", gp, "-q", qp, "-gn", "1", "--algo", "cpu"],
+             {"PYTHONPATH": ROOT})
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[2] == "Query number (k) with minimum F value: 2" and lines[3] == "Minimum F value: 3"
+    r = _run([sys.executable, "-m", "msbfs", "-g"], {"PYTHONPATH": ROOT})
+    assert r.returncode == 255 and "Usage" in r.stderr

@@ -1,0 +1,71 @@
+"""Multi-process (gloo, CPU) coverage of the torch.distributed layer and the end-to-end engine:
+every world size must produce the identical report (round-robin invariance, main.cu:305)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, gp, qp, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import msbfs
+    from msbfs.parallel import distributed as D
+    ctx = D.init_from_env(backend="gloo", use_gpu=False)
+    assert ctx.world == world and ctx.rank == rank
+    # primitives
+    qs = msbfs.QuerySet.from_file(qp) if rank == 0 else None
+    qs = D.broadcast_queries(qs, ctx)
+    g = msbfs.Graph.from_file(gp) if rank == 0 else None
+    g = D.broadcast_graph(g, ctx)
+    idx = D.round_robin(qs.K, rank, world)
+    r = msbfs.cpu_bfs(g, qs.subset(idx), count_edges=True)
+    k, f = D.packed_argmin(r.F, idx, qs.K, ctx)
+    F = D.gather_F(r.F, idx, qs.K, ctx)
+    # end-to-end engine
+    eng = msbfs.Engine(msbfs.JobConfig(graph=gp, query=qp, algo="cpu", count_edges=True), ctx)
+    eng.preprocess()
+    res = eng.compute(gather=True)
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), k=k, f=f, F=F, ek=res.min_k, ef=res.min_f,
+             eF=res.F, edges=res.traversed_edges, n=g.n)
+    D.shutdown(ctx)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_gloo_world_sizes(tmp_path, msbfs_pkg, world):
+    m = msbfs_pkg
+    g = m.Graph.rmat(10, 8, 1)
+    qs = m.QuerySet.random(g.n, 7, 3, 2)
+    gp, qp = str(tmp_path / "g.bin"), str(tmp_path / "q.bin")
+    g.write(gp)
+    qs.write(qp)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    mp.spawn(_worker, args=(world, _free_port(), gp, qp, str(tmp_path)), nprocs=world, join=True)
+    k = m.argmin_first(ref.F)
+    for r in range(world):
+        z = np.load(tmp_path / f"r{r}.npz")
+        assert int(z["n"]) == g.n
+        assert int(z["k"]) == k and int(z["f"]) == ref.F[k]
+        assert int(z["ek"]) == k and int(z["ef"]) == ref.F[k]
+        assert np.array_equal(z["F"], ref.F) and np.array_equal(z["eF"], ref.F)
+        assert int(z["edges"]) == int(ref.edges.sum())
+
+
+def test_packed_argmin_tiebreak_and_fallback():
+    from msbfs.parallel import distributed as D
+    ctx = D.DistContext()
+    assert D.packed_argmin(np.array([5, 3, 3, 9]), np.array([0, 1, 2, 3]), 4, ctx) == (1, 3)
+    assert D.packed_argmin(np.array([], np.int64), np.array([], np.int64), 0, ctx) == (-1, -1)
+    big = np.array([2 ** 61, 2 ** 61, 2 ** 62], np.int64)  # too large to pack next to q
+    assert D.packed_argmin(big, np.array([7, 3, 1]), 8, ctx) == (3, 2 ** 61)
+    assert list(D.round_robin(10, 2, 4)) == [2, 6]

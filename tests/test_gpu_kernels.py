@@ -121,3 +121,20 @@ def test_device_uniform_and_wrap(msbfs_pkg):
     qs = m.QuerySet.random(hg.n, 50, 4, 1)
     with m.Solver(wg, "bitpar", max_groups=50) as s:
         assert np.array_equal(s.run(qs).F, m.cpu_bfs(hg, qs).F)
+
+
+@pytest.mark.parametrize("scale,K", [(16, 1024), (18, 700)])
+def test_bitpar_large_rmat_vs_cpu(msbfs_pkg, scale, K):
+    """Large enough that every block runs many tiles and flushes its LDS queues repeatedly:
+    catches LDS init/flush races that 1-block toy graphs cannot."""
+    m = msbfs_pkg
+    dg = m.DeviceGraph.rmat(scale, 16, 3, device=0)
+    qs = m.QuerySet.random(dg.n, K, 16, seed=scale)
+    ref = m.cpu_bfs(dg.download(), qs, count_edges=True)
+    with m.Solver(dg, "bitpar", max_groups=K) as s:
+        for _ in range(2):
+            r = s.run(qs, count_edges=True)
+            assert np.array_equal(r.F, ref.F)
+            assert np.array_equal(r.edges, ref.edges)
+    with m.Solver(dg, "dist") as s:
+        assert np.array_equal(s.run(qs.subset(range(8))).F, ref.F[:8])
