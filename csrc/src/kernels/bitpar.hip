@@ -44,6 +44,7 @@ constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr int kQCap = 1024;       // LDS queue capacity (items) per block
 constexpr int kChunk = 1024;      // bottom-up edge chunk for wide vertices
+constexpr int kMaxGrid = 2048;    // blocks of the grid-stride level kernels
 
 template <int W>
 struct Lay {
@@ -205,20 +206,99 @@ __device__ __forceinline__ void count_bits(Lds<W, COUNT>& s, const V<Lay<W>::VW>
   }
 }
 
+// Per-block counter row -> slab row blockIdx.x (plain stores; no same-address atomics). The
+// level's rows are summed by k_level_reduce.
 template <int W, bool COUNT>
-__device__ __forceinline__ void lds_flush(Lds<W, COUNT>& s, unsigned long long* F,
-                                          unsigned long long* E, uint64_t* alive_next,
-                                          uint32_t level) {
+__device__ __forceinline__ void slab_store(Lds<W, COUNT>& s, uint32_t* slabF,
+                                           unsigned long long* slabE) {
   __syncthreads();
+  uint32_t* rf = slabF + (size_t)blockIdx.x * (64 * W);
   for (int i = threadIdx.x; i < 64 * W; i += blockDim.x) {
-    const uint32_t c = s.f[i];
-    if (c) {
-      atomicAdd(&F[i], (unsigned long long)c * level);
-      atomicOr((unsigned long long*)&alive_next[i >> 6], 1ull << (i & 63));
+    rf[i] = s.f[i];
+    if constexpr (COUNT) slabE[(size_t)blockIdx.x * (64 * W) + i] = s.e[i];
+  }
+}
+
+// Register-resident bit-sliced (carry-save) counters: bit b of c[j][d] is bit d of the count of
+// group (slot*VW + j)*64 + b. Adding a 64-bit new-bits word costs 2*D branch-free ops, vs one
+// LDS atomic per set bit in a divergent loop. Spilled to LDS every < 2^D additions.
+template <int VW>
+struct BitCounter {
+  static constexpr int D = 7;
+  uint64_t c[VW][D];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int j = 0; j < VW; ++j)
+#pragma unroll
+      for (int d = 0; d < D; ++d) c[j][d] = 0;
+  }
+  __device__ __forceinline__ void add(const V<VW>& x) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      uint64_t carry = x.w[j];
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const uint64_t t = c[j][d] & carry;
+        c[j][d] ^= carry;
+        carry = t;
+      }
     }
+  }
+  template <int W, bool COUNT>
+  __device__ __forceinline__ void spill(Lds<W, COUNT>& s, int slot) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      uint64_t any = 0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) any |= c[j][d];
+      const int base = (slot * VW + j) * 64;
+      while (any) {
+        const int b = __ffsll((unsigned long long)any) - 1;
+        any &= any - 1;
+        uint32_t v = 0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) v |= (uint32_t)((c[j][d] >> b) & 1ull) << d;
+        atomicAdd(&s.f[base + b], v);
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) c[j][d] = 0;
+    }
+  }
+};
+
+// Sum the level's slab rows: block (word, row-group); lane = group bit. F += level * count,
+// alive_next |= groups with count > 0 (one ballot + one atomicOr per word per row-group).
+template <int W, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
+                                                         const unsigned long long* slabE, int rows,
+                                                         int rgroups, unsigned long long* F,
+                                                         unsigned long long* E,
+                                                         uint64_t* alive_next, uint32_t level) {
+  __shared__ unsigned long long pf[kWaves][64], pe[kWaves][64];
+  const int word = blockIdx.x % W, rg = blockIdx.x / W;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  const int r0 = (int)((int64_t)rows * rg / rgroups);
+  const int r1 = (int)((int64_t)rows * (rg + 1) / rgroups);
+  const int i = word * 64 + lane;
+  unsigned long long f = 0, e = 0;
+  for (int r = r0 + wv; r < r1; r += kWaves) {
+    f += slabF[(size_t)r * (64 * W) + i];
+    if constexpr (COUNT) e += slabE[(size_t)r * (64 * W) + i];
+  }
+  pf[wv][lane] = f;
+  pe[wv][lane] = e;
+  __syncthreads();
+  if (wv == 0) {
+    for (int w = 1; w < kWaves; ++w) {
+      f += pf[w][lane];
+      e += pe[w][lane];
+    }
+    if (f) atomicAdd(&F[i], f * level);
     if constexpr (COUNT) {
-      if (s.e[i]) atomicAdd(&E[i], s.e[i]);
+      if (e) atomicAdd(&E[i], e);
     }
+    const uint64_t m = __ballot(f != 0);
+    if (lane == 0 && m) atomicOr((unsigned long long*)&alive_next[word], m);
   }
 }
 
@@ -327,8 +407,8 @@ template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_td_finalize(
     const int32_t* touched, const int64_t* rowptr, uint64_t* visCur, uint64_t* visOld,
     uint64_t* accNext, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* fl2,
-    Ctr* ctr, unsigned long long* F, unsigned long long* E, uint64_t* alive_next, uint32_t level,
-    const int32_t* fl_old, int64_t nf_old, uint64_t* accCur_zero) {
+    Ctr* ctr, uint32_t* slabF, unsigned long long* slabE, const int32_t* fl_old, int64_t nf_old,
+    uint64_t* accCur_zero) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ Lds<W, COUNT> s;
@@ -347,6 +427,9 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
     gm.w[j] = gmask[slot * VW + j];
   }
   unsigned long long ef = 0;
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
   for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nt; tb += (int64_t)gridDim.x * TILE) {
     const int64_t idx = tb + wv * VPW + sub;
     const bool valid = idx < nt;
@@ -379,7 +462,15 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
     if (leader && g_full) set_done(done, v);
     const bool app = leader && g_new;
     if (app) ef += deg;
-    if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
+    if constexpr (COUNT) {
+      if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
+    } else {
+      bc.add(nw);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.spill(s, slot);
+        nadd = 0;
+      }
+    }
     q_push(q, app, v);
     q_flush(q, fl2, &ctr->fl2.v, TILE, false);
   }
@@ -394,7 +485,8 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
       if (idx < nf_old) stv<VW>(accCur_zero + (int64_t)fl_old[idx] * W + slot * VW, vzero<VW>());
     }
   }
-  lds_flush<W, COUNT>(s, F, E, alive_next, level);
+  if constexpr (!COUNT) bc.spill(s, slot);
+  slab_store<W, COUNT>(s, slabF, slabE);
 }
 
 template <int W>
@@ -447,8 +539,7 @@ template <int W, bool COUNT, int U>
 __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
-    int32_t* act2, int32_t* fl2, Ctr* ctr, unsigned long long* F, unsigned long long* E,
-    uint64_t* alive_next, uint32_t level) {
+    int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* slabF, unsigned long long* slabE) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ Lds<W, COUNT> s;
@@ -464,6 +555,9 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long eu = 0, ef = 0;
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
   for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nact; tb += (int64_t)gridDim.x * TILE) {
     const int64_t idx = tb + wv * VPW + sub;
     const bool valid = idx < nact;
@@ -528,7 +622,15 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     const bool keep = leader && g_nf, app = leader && g_new;
     if (keep) eu += deg;
     if (app) ef += deg;
-    if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
+    if constexpr (COUNT) {
+      if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
+    } else {
+      bc.add(nw);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.spill(s, slot);
+        nadd = 0;
+      }
+    }
     q_push(qa, keep, v);
     q_push(qf, app, v);
     q_flush(qa, act2, &ctr->act2.v, TILE, false);
@@ -538,7 +640,8 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
   q_flush(qf, fl2, &ctr->fl2.v, 0, true);
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
-  lds_flush<W, COUNT>(s, F, E, alive_next, level);
+  if constexpr (!COUNT) bc.spill(s, slot);
+  slab_store<W, COUNT>(s, slabF, slabE);
 }
 
 // bottom-up, wide vertices, phase 1: one wave per edge chunk (<= kChunk edges). S = 64/G
@@ -614,8 +717,7 @@ template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, uint64_t* Wb,
     uint64_t* acc, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* actw2,
-    int32_t* fl2, Ctr* ctr, unsigned long long* F, unsigned long long* E, uint64_t* alive_next,
-    uint32_t level) {
+    int32_t* fl2, Ctr* ctr, uint32_t* slabF, unsigned long long* slabE) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ Lds<W, COUNT> s;
@@ -631,6 +733,9 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long eu = 0, ef = 0;
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
   for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nw; tb += (int64_t)gridDim.x * TILE) {
     const int64_t idx = tb + wv * VPW + sub;
     const bool valid = idx < nw;
@@ -664,7 +769,15 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const bool keep = leader && g_nf, app = leader && g_new;
     if (keep) eu += deg;
     if (app) ef += deg;
-    if (anynew) count_bits<W, COUNT>(s, nwb, slot, deg);
+    if constexpr (COUNT) {
+      if (anynew) count_bits<W, COUNT>(s, nwb, slot, deg);
+    } else {
+      bc.add(nwb);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.spill(s, slot);
+        nadd = 0;
+      }
+    }
     q_push(qa, keep, v);
     q_push(qf, app, v);
     q_flush(qa, actw2, &ctr->actw2.v, TILE, false);
@@ -674,7 +787,8 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
   q_flush(qf, fl2, &ctr->fl2.v, 0, true);
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
-  lds_flush<W, COUNT>(s, F, E, alive_next, level);
+  if constexpr (!COUNT) bc.spill(s, slot);
+  slab_store<W, COUNT>(s, slabF, slabE);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -707,6 +821,9 @@ class BitparSolver final : public Solver {
     scan_tmp_.alloc(scan_bytes_);
     ctr_.alloc(sizeof(Ctr));
     small_.alloc(64 * 16 * sizeof(unsigned long long) * 2 + 4 * 16 * sizeof(uint64_t));
+    // per-level counter slab: <= 3 counting kernels per level x <= kMaxGrid blocks
+    slabF_.alloc((size_t)3 * kMaxGrid * 64 * maxW_ * sizeof(uint32_t));
+    slabE_.alloc((size_t)3 * kMaxGrid * 64 * maxW_ * sizeof(unsigned long long));
     hctr_ = std::make_unique<PinnedBuf>(sizeof(Ctr));
     if (const char* d = getenv("MSBFS_DIRS")) dirs_ = d;  // per-level T/B override (tuning)
     if (const char* u = getenv("MSBFS_UNROLL")) unroll_ = atoi(u);
@@ -761,7 +878,7 @@ class BitparSolver final : public Solver {
   const DeviceGraph& g_;
   int maxW_ = 1;
   DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
-      ctr_, small_, pairs_;
+      ctr_, small_, pairs_, slabF_, slabE_;
   size_t scan_bytes_ = 0;
   std::unique_ptr<PinnedBuf> hctr_;
   int32_t epoch_ = 0;
@@ -829,7 +946,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
   bool have_active = false, fsrc_acc = true, bottom_up = false;
   int alv = 0;
   uint32_t level = 0;
-  const int grid = 2048;
+  const int grid = kMaxGrid;
   static const bool trace = getenv("MSBFS_TRACE") != nullptr;
   auto tl = std::chrono::steady_clock::now();
   while (nf > 0) {
@@ -843,6 +960,9 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
     MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
     MSBFS_HIP_CHECK(hipMemsetAsync(alive[alv ^ 1], 0, 16 * sizeof(uint64_t), s));
     ++level;
+    int rows = 0;  // slab rows written by this level's counting kernels
+    auto slabF = [&](int r) { return slabF_.as<uint32_t>() + (size_t)r * 64 * W; };
+    auto slabE = [&](int r) { return slabE_.as<unsigned long long>() + (size_t)r * 64 * W; };
     uint64_t* R = vis_[cur].as<uint64_t>();
     uint64_t* O = vis_[cur ^ 1].as<uint64_t>();
     if (!bottom_up) {
@@ -864,11 +984,12 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
       MSBFS_HIP_CHECK(hipGetLastError());
       // touched <= min(n, frontier edges); the kernel reads the exact count from ctr
       const int64_t nt_max = std::min<int64_t>(std::max<int64_t>(ef, nf), n);
-      k_td_finalize<W, COUNT><<<grid_for(nt_max, L::TILE, grid), kBlock, 0, s>>>(
+      const int gf = grid_for(nt_max, L::TILE, grid);
+      k_td_finalize<W, COUNT><<<gf, kBlock, 0, s>>>(
           touched_.as<int32_t>(), g_.rowptr, R, O, acc_[ac ^ 1].as<uint64_t>(), alive[alv],
-          gmask, done_.as<uint32_t>(), fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), dF, dE,
-          alive[alv ^ 1], level, fl_[fc].as<int32_t>(), nf,
-          fsrc_acc ? acc_[ac].as<uint64_t>() : nullptr);
+          gmask, done_.as<uint32_t>(), fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), slabF(rows),
+          slabE(rows), fl_[fc].as<int32_t>(), nf, fsrc_acc ? acc_[ac].as<uint64_t>() : nullptr);
+      rows += gf;
       MSBFS_HIP_CHECK(hipGetLastError());
       ac ^= 1;
       fsrc_acc = true;
@@ -895,10 +1016,12 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
       }
       if (nact) {
         auto kern = unroll_ >= 8 ? k_bu_narrow<W, COUNT, 8> : k_bu_narrow<W, COUNT, 4>;
-        kern<<<grid_for(nact, L::TILE, grid), kBlock, 0, s>>>(
-            act_[0].as<int32_t>(), nact, g_.rowptr, g_.col, R, O, alive[alv], gmask,
-            done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
-            ctr_.as<Ctr>(), dF, dE, alive[alv ^ 1], level);
+        const int gn = grid_for(nact, L::TILE, grid);
+        kern<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), nact, g_.rowptr, g_.col, R, O, alive[alv],
+                                   gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
+                                   fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), slabF(rows),
+                                   slabE(rows));
+        rows += gn;
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       if (nactw) {
@@ -909,10 +1032,12 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
             actw_[0].as<int32_t>(), nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
             alive[alv], gmask, acc_[ac].as<uint64_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
-        k_bu_wide_finalize<W, COUNT><<<grid_for(nactw, L::TILE, grid), kBlock, 0, s>>>(
+        const int gw = grid_for(nactw, L::TILE, grid);
+        k_bu_wide_finalize<W, COUNT><<<gw, kBlock, 0, s>>>(
             actw_[0].as<int32_t>(), nactw, g_.rowptr, R, O, acc_[ac].as<uint64_t>(), alive[alv],
             gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
-            ctr_.as<Ctr>(), dF, dE, alive[alv ^ 1], level);
+            ctr_.as<Ctr>(), slabF(rows), slabE(rows));
+        rows += gw;
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       std::swap(act_[0], act_[1]);
@@ -920,6 +1045,12 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
       cur ^= 1;
       fsrc_acc = false;
       if (st) st->bu_levels++;
+    }
+    if (rows) {
+      const int rg = std::max(1, std::min(64, rows / 32));
+      k_level_reduce<W, COUNT><<<W * rg, kBlock, 0, s>>>(slabF(0), slabE(0), rows, rg, dF, dE,
+                                                         alive[alv ^ 1], level);
+      MSBFS_HIP_CHECK(hipGetLastError());
     }
     c = read_ctr(s);
     if (bottom_up) {
