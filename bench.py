@@ -47,6 +47,8 @@ def main() -> int:
     ap.add_argument("--beta", type=float, default=0.0)
     ap.add_argument("--wide-degree", type=int, default=0)
     ap.add_argument("--max-words", type=int, default=0)
+    ap.add_argument("--relabel", type=int, default=1,
+                    help="renumber vertices by descending degree after generation (preprocessing)")
     args = ap.parse_args()
 
     import torch
@@ -57,7 +59,8 @@ def main() -> int:
     ctx = D.init_from_env(use_gpu=True)
     dev = ctx.device
     t_setup = time.perf_counter()
-    g = msbfs.DeviceGraph.rmat(args.scale, args.edgefactor, args.seed, device=dev)
+    g = msbfs.DeviceGraph.rmat(args.scale, args.edgefactor, args.seed, device=dev,
+                               relabel=bool(args.relabel))
     qs = msbfs.QuerySet.random(g.n, args.groups, args.group_size, args.qseed)
     local_idx = D.round_robin(qs.K, ctx.rank, ctx.world)
     local_q = qs.subset(local_idx)
@@ -119,7 +122,7 @@ def main() -> int:
                 "min_k": int(min_k) + 1, "min_f": int(min_f),
                 "levels": stats.get("levels"), "td_levels": stats.get("td_levels"),
                 "bu_levels": stats.get("bu_levels"), "batches": stats.get("batches"),
-                "setup_s": round(setup_s, 3),
+                "setup_s": round(setup_s, 3), "relabel": bool(args.relabel),
             },
         }
         print(json.dumps(out), flush=True)

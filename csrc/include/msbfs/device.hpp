@@ -74,6 +74,10 @@ struct DeviceGraph {
   DevBuf own_rowptr, own_col;
   int64_t max_degree = 0;
   int64_t isolated = 0;
+  // Optional degree-descending relabelling: old2new[v] maps a user vertex id to the internal id
+  // (null when the graph keeps the user's ids). Solvers map query sources through it.
+  int32_t* old2new = nullptr;
+  DevBuf own_old2new;
 };
 
 // Stats returned by solvers (mirrors msbfs_stats in msbfs.h).
@@ -92,6 +96,9 @@ void device_graph_gen_rmat(DeviceGraph& g, int scale, int64_t edgefactor, uint64
 void device_graph_gen_uniform(DeviceGraph& g, int64_t n, int64_t m, uint64_t seed, hipStream_t s);
 void device_graph_stats(DeviceGraph& g, hipStream_t s);
 void device_graph_sort_rows(DeviceGraph& g, hipStream_t s);
+// Renumber vertices by descending degree (stable), rebuild the CSR with sorted rows and keep the
+// old->new map in g.old2new. F(U) is invariant under relabelling.
+void device_graph_relabel_by_degree(DeviceGraph& g, hipStream_t s);
 
 // ---- solvers ---------------------------------------------------------------------------------
 struct SolverOptions {

@@ -81,6 +81,11 @@ int msbfs_graph_gen_rmat(int device, int scale, int64_t edgefactor, uint64_t see
                          double b, double c, int scramble, msbfs_graph* out);
 int msbfs_graph_gen_uniform(int device, int64_t n, int64_t m, uint64_t seed, msbfs_graph* out);
 int msbfs_graph_sort_rows(msbfs_graph g);
+/* Renumber vertices by descending degree (hubs first, rows sorted). Queries keep using the
+ * original ids: solvers map sources through the stored old->new map. */
+int msbfs_graph_relabel_by_degree(msbfs_graph g);
+int msbfs_graph_relabel_map(msbfs_graph g, int32_t* old2new);
+int msbfs_graph_is_relabelled(msbfs_graph g);
 int msbfs_graph_info(msbfs_graph g, int64_t* n, int64_t* nnz, int64_t* m, int64_t* max_degree,
                      int64_t* isolated);
 int msbfs_graph_device_ptrs(msbfs_graph g, void** rowptr, void** col);

@@ -256,6 +256,24 @@ int msbfs_graph_sort_rows(msbfs_graph g) {
   });
 }
 
+int msbfs_graph_relabel_by_degree(msbfs_graph g) {
+  return guard([&] {
+    MSBFS_HIP_CHECK(hipSetDevice(g->g.device));
+    msbfs::device_graph_relabel_by_degree(g->g, nullptr);
+  });
+}
+
+int msbfs_graph_relabel_map(msbfs_graph g, int32_t* old2new) {
+  return guard([&] {
+    if (!g->g.old2new) msbfs::fail("graph is not relabelled");
+    MSBFS_HIP_CHECK(hipSetDevice(g->g.device));
+    MSBFS_HIP_CHECK(hipMemcpy(old2new, g->g.old2new, g->g.n * sizeof(int32_t),
+                              hipMemcpyDeviceToHost));
+  });
+}
+
+int msbfs_graph_is_relabelled(msbfs_graph g) { return g->g.old2new ? 1 : 0; }
+
 int msbfs_graph_info(msbfs_graph g, int64_t* n, int64_t* nnz, int64_t* m, int64_t* max_degree,
                      int64_t* isolated) {
   return guard([&] {

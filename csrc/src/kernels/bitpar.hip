@@ -106,11 +106,12 @@ struct Ctr {
   Slot32 act2, actw2, fl2, touched;
   Slot64 ef2;  // sum of degrees of the next frontier
   Slot64 eu2;  // sum of degrees of the next active lists
+  Slot64 ev2;  // sum of degrees of vertices visited for the first time (by any group)
 };
 // host view of the interesting fields
 struct HostCtr {
   uint32_t act2, actw2, fl2, touched;
-  unsigned long long ef2, eu2;
+  unsigned long long ef2, eu2, ev2;
 };
 
 __device__ __forceinline__ bool is_done(const uint32_t* done, int32_t v) {
@@ -118,6 +119,12 @@ __device__ __forceinline__ bool is_done(const uint32_t* done, int32_t v) {
 }
 __device__ __forceinline__ void set_done(uint32_t* done, int32_t v) {
   atomicOr(&done[v >> 5], 1u << (v & 31));
+}
+// anyvis: bit v set once vertex v is visited by any group. A clear bit guarantees both visited
+// buffers of v are all-zero (bits are set before/with the first non-zero store and never
+// cleared within a batch), so pulls may skip the 8*W-byte load; a set bit only costs a load.
+__device__ __forceinline__ bool any_visited(const uint32_t* anyvis, int32_t u) {
+  return (anyvis[u >> 5] >> (u & 31)) & 1u;
 }
 
 // ---- per-block LDS queues ---------------------------------------------------------------------
@@ -311,7 +318,8 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_
                                                  const int64_t* rowptr, uint64_t* visA,
                                                  uint64_t* visB, uint64_t* acc, int32_t* stamp,
                                                  int32_t epoch, int32_t* fl, Ctr* ctr,
-                                                 unsigned long long* E, uint64_t* alive) {
+                                                 unsigned long long* E, uint64_t* alive,
+                                                 uint32_t* anyvis, const int32_t* relabel) {
   __shared__ LdsQueue q;
   __shared__ unsigned long long scratch[kWaves];
   q_init(q);
@@ -323,6 +331,7 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_
     int32_t v = 0;
     if (i < np) {
       v = pv[i];
+      if (relabel) v = relabel[v];  // user id -> internal (degree-ordered) id
       const int k = pk[i];
       const int word = k >> 6;
       const uint64_t bit = 1ull << (k & 63);
@@ -334,7 +343,10 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_
         const unsigned long long deg = (unsigned long long)(rowptr[v + 1] - rowptr[v]);
         if constexpr (COUNT) atomicAdd(&E[k], deg);
         app = atomicExch(&stamp[v], epoch) != epoch;
-        if (app) ef += deg;
+        if (app) {
+          ef += deg;
+          atomicOr(&anyvis[v >> 5], 1u << (v & 31));
+        }
       }
     }
     q_push(q, app, v);
@@ -342,6 +354,7 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_
   }
   q_flush(q, fl, &ctr->fl2.v, 0, true);
   block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ef, &ctr->ev2.v, scratch);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -407,14 +420,12 @@ template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_td_finalize(
     const int32_t* touched, const int64_t* rowptr, uint64_t* visCur, uint64_t* visOld,
     uint64_t* accNext, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* fl2,
-    Ctr* ctr, uint32_t* slabF, unsigned long long* slabE, const int32_t* fl_old, int64_t nf_old,
-    uint64_t* accCur_zero) {
+    Ctr* ctr, const int32_t* fl_old, int64_t nf_old,
+    uint64_t* accCur_zero, uint32_t* anyvis) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
-  __shared__ Lds<W, COUNT> s;
   __shared__ LdsQueue q;
   __shared__ unsigned long long scratch[kWaves];
-  lds_zero(s);
   q_init(q);
   __syncthreads();
   const int64_t nt = ctr->touched.v;  // written by k_td_expand (previous kernel on the stream)
@@ -426,15 +437,12 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
     am.w[j] = alive[slot * VW + j];
     gm.w[j] = gmask[slot * VW + j];
   }
-  unsigned long long ef = 0;
-  BitCounter<VW> bc;
-  bc.zero();
-  int nadd = 0;
+  unsigned long long ef = 0, ev = 0;
   for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nt; tb += (int64_t)gridDim.x * TILE) {
     const int64_t idx = tb + wv * VPW + sub;
     const bool valid = idx < nt;
     int32_t v = 0;
-    bool anynew = false, notfull = false;
+    bool anynew = false, notfull = false, rnz = false;
     V<VW> nw = vzero<VW>();
     uint32_t deg = 0;
     if (valid) {
@@ -449,33 +457,31 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
         nv.w[j] = r.w[j] | nw.w[j];
         anynew |= nw.w[j] != 0;
         notfull |= (~nv.w[j] & am.w[j] & gm.w[j]) != 0;
+        rnz |= r.w[j] != 0;
       }
       stv<VW>(accNext + vo, nw);
       stv<VW>(visCur + vo, nv);
       stv<VW>(visOld + vo, nv);
       deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
     }
-    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
+    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull), br = __ballot(rnz);
     const bool g_new = (bn >> (sub * G)) & L::GBITS;
     const bool g_full = !((bf >> (sub * G)) & L::GBITS);
+    const bool g_first = g_new && !((br >> (sub * G)) & L::GBITS);
     const bool leader = valid && slot == 0;
     if (leader && g_full) set_done(done, v);
     const bool app = leader && g_new;
     if (app) ef += deg;
-    if constexpr (COUNT) {
-      if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
-    } else {
-      bc.add(nw);
-      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
-        bc.spill(s, slot);
-        nadd = 0;
-      }
+    if (leader && g_first) {
+      atomicOr(&anyvis[v >> 5], 1u << (v & 31));
+      ev += deg;
     }
     q_push(q, app, v);
     q_flush(q, fl2, &ctr->fl2.v, TILE, false);
   }
   q_flush(q, fl2, &ctr->fl2.v, 0, true);
   block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
   // zero the consumed top-down frontier bits of the previous frontier
   if (accCur_zero) {
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -485,8 +491,6 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
       if (idx < nf_old) stv<VW>(accCur_zero + (int64_t)fl_old[idx] * W + slot * VW, vzero<VW>());
     }
   }
-  if constexpr (!COUNT) bc.spill(s, slot);
-  slab_store<W, COUNT>(s, slabF, slabE);
 }
 
 template <int W>
@@ -539,13 +543,11 @@ template <int W, bool COUNT, int U>
 __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
-    int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* slabF, unsigned long long* slabE) {
+    int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int filter) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
-  __shared__ Lds<W, COUNT> s;
   __shared__ LdsQueue qa, qf;
   __shared__ unsigned long long scratch[kWaves];
-  lds_zero(s);
   q_init(qa);
   q_init(qf);
   __syncthreads();
@@ -554,16 +556,13 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  unsigned long long eu = 0, ef = 0;
-  BitCounter<VW> bc;
-  bc.zero();
-  int nadd = 0;
+  unsigned long long eu = 0, ef = 0, ev = 0;
   for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nact; tb += (int64_t)gridDim.x * TILE) {
     const int64_t idx = tb + wv * VPW + sub;
     const bool valid = idx < nact;
     int32_t v = 0;
     V<VW> r = vzero<VW>(), unv = vzero<VW>(), acc = vzero<VW>();
-    bool lane_open = false;
+    bool lane_open = false, rnz = false;
     int64_t beg = 0, end = 0;
     if (valid) {
       v = act[idx];
@@ -572,6 +571,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
       for (int j = 0; j < VW; ++j) {
         unv.w[j] = ~r.w[j] & am.w[j];
         lane_open |= unv.w[j] != 0;
+        rnz |= r.w[j] != 0;
       }
       beg = rowptr[v];
       end = rowptr[v + 1];
@@ -583,6 +583,11 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
         int32_t u[U];
 #pragma unroll
         for (int q = 0; q < U; ++q) u[q] = (e + q < end) ? col[e + q] : -1;
+        if (filter) {
+#pragma unroll
+          for (int q = 0; q < U; ++q)
+            if (u[q] >= 0 && !any_visited(anyvis, u[q])) u[q] = -1;
+        }
         V<VW> x[U];
 #pragma unroll
         for (int q = 0; q < U; ++q)
@@ -622,13 +627,11 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     const bool keep = leader && g_nf, app = leader && g_new;
     if (keep) eu += deg;
     if (app) ef += deg;
-    if constexpr (COUNT) {
-      if (anynew) count_bits<W, COUNT>(s, nw, slot, deg);
-    } else {
-      bc.add(nw);
-      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
-        bc.spill(s, slot);
-        nadd = 0;
+    {
+      const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
+      if (leader && g_first) {
+        atomicOr(&anyvis[v >> 5], 1u << (v & 31));
+        ev += deg;
       }
     }
     q_push(qa, keep, v);
@@ -640,8 +643,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
   q_flush(qf, fl2, &ctr->fl2.v, 0, true);
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
-  if constexpr (!COUNT) bc.spill(s, slot);
-  slab_store<W, COUNT>(s, slabF, slabE);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
 }
 
 // bottom-up, wide vertices, phase 1: one wave per edge chunk (<= kChunk edges). S = 64/G
@@ -650,7 +652,8 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_bu_chunks(
     const int32_t* wl, int64_t nw, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
-    const uint64_t* R, const uint64_t* alive, const uint64_t* gmask, uint64_t* acc) {
+    const uint64_t* R, const uint64_t* alive, const uint64_t* gmask, uint64_t* acc,
+    const uint32_t* anyvis, int filter) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
@@ -685,6 +688,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
       for (int q = 0; q < 4; ++q) {
         const int64_t e = e0 + sub + (int64_t)q * S;
         u[q] = e < lim ? col[e] : -1;
+        if (filter && u[q] >= 0 && !any_visited(anyvis, u[q])) u[q] = -1;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -717,13 +721,11 @@ template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, uint64_t* Wb,
     uint64_t* acc, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* actw2,
-    int32_t* fl2, Ctr* ctr, uint32_t* slabF, unsigned long long* slabE) {
+    int32_t* fl2, Ctr* ctr, uint32_t* anyvis) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
-  __shared__ Lds<W, COUNT> s;
   __shared__ LdsQueue qa, qf;
   __shared__ unsigned long long scratch[kWaves];
-  lds_zero(s);
   q_init(qa);
   q_init(qf);
   __syncthreads();
@@ -732,16 +734,13 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  unsigned long long eu = 0, ef = 0;
-  BitCounter<VW> bc;
-  bc.zero();
-  int nadd = 0;
+  unsigned long long eu = 0, ef = 0, ev = 0;
   for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nw; tb += (int64_t)gridDim.x * TILE) {
     const int64_t idx = tb + wv * VPW + sub;
     const bool valid = idx < nw;
     int32_t v = 0;
     V<VW> nwb = vzero<VW>();
-    bool anynew = false, notfull = false;
+    bool anynew = false, notfull = false, rnz = false;
     uint32_t deg = 0;
     if (valid) {
       v = wl[idx];
@@ -756,6 +755,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
         nv.w[j] = r.w[j] | nwb.w[j];
         anynew |= nwb.w[j] != 0;
         notfull |= (unv & ~nwb.w[j]) != 0;
+        rnz |= r.w[j] != 0;
       }
       stv<VW>(acc + vo, vzero<VW>());
       stv<VW>(Wb + vo, nv);
@@ -769,13 +769,11 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const bool keep = leader && g_nf, app = leader && g_new;
     if (keep) eu += deg;
     if (app) ef += deg;
-    if constexpr (COUNT) {
-      if (anynew) count_bits<W, COUNT>(s, nwb, slot, deg);
-    } else {
-      bc.add(nwb);
-      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
-        bc.spill(s, slot);
-        nadd = 0;
+    {
+      const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
+      if (leader && g_first) {
+        atomicOr(&anyvis[v >> 5], 1u << (v & 31));
+        ev += deg;
       }
     }
     q_push(qa, keep, v);
@@ -787,6 +785,58 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
   q_flush(qf, fl2, &ctr->fl2.v, 0, true);
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-level accounting, once per level over the NEW frontier list (kept out of the traversal
+// kernels so they keep their occupancy): new bits of v = visNew[v] & ~visOld[v] after a
+// bottom-up level (DIFF) or acc[v] after a top-down level. G lanes per vertex; counts go to
+// register bit-sliced counters (or, for the edge-count mode, per-bit LDS atomics weighted by
+// degree), then to this block's slab row.
+// ---------------------------------------------------------------------------------------------
+template <int W, bool COUNT, bool DIFF>
+__global__ __launch_bounds__(kBlock) void k_count_frontier(const int32_t* fl, const Ctr* ctr,
+                                                           const int64_t* rowptr,
+                                                           const uint64_t* a,
+                                                           const uint64_t* b, uint32_t* slabF,
+                                                           unsigned long long* slabE) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  __shared__ Lds<W, COUNT> s;
+  lds_zero(s);
+  __syncthreads();
+  const int64_t nf = ctr->fl2.v;
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nf; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t idx = tb + wv * VPW + sub;
+    V<VW> nw = vzero<VW>();
+    uint32_t deg = 0;
+    if (idx < nf) {
+      const int32_t v = fl[idx];
+      const int64_t vo = (int64_t)v * W + slot * VW;
+      nw = ldv<VW>(a + vo);
+      if constexpr (DIFF) {
+        const V<VW> o = ldv<VW>(b + vo);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) nw.w[j] &= ~o.w[j];
+      }
+      if constexpr (COUNT) deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
+    }
+    if constexpr (COUNT) {
+      count_bits<W, COUNT>(s, nw, slot, deg);
+    } else {
+      bc.add(nw);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.spill(s, slot);
+        nadd = 0;
+      }
+    }
+  }
   if constexpr (!COUNT) bc.spill(s, slot);
   slab_store<W, COUNT>(s, slabF, slabE);
 }
@@ -810,6 +860,8 @@ class BitparSolver final : public Solver {
     stamp_.alloc((size_t)n * sizeof(int32_t));
     MSBFS_HIP_CHECK(hipMemset(stamp_.p, 0xFF, stamp_.bytes));
     done_.alloc((size_t)((n + 31) / 32) * sizeof(uint32_t));
+    anyvis_.alloc((size_t)((n + 31) / 32) * sizeof(uint32_t));
+    if (const char* f = getenv("MSBFS_FILTER_FRAC")) filter_frac_ = atof(f);
     for (int i = 0; i < 2; ++i) {
       act_[i].alloc((size_t)n * sizeof(int32_t));
       actw_[i].alloc((size_t)n * sizeof(int32_t));
@@ -872,18 +924,19 @@ class BitparSolver final : public Solver {
     MSBFS_HIP_CHECK(hipMemcpyAsync(hctr_->p, ctr_.p, sizeof(Ctr), hipMemcpyDeviceToHost, s));
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
     const Ctr* c = hctr_->as<Ctr>();
-    return HostCtr{c->act2.v, c->actw2.v, c->fl2.v, c->touched.v, c->ef2.v, c->eu2.v};
+    return HostCtr{c->act2.v, c->actw2.v, c->fl2.v, c->touched.v, c->ef2.v, c->eu2.v, c->ev2.v};
   }
 
   const DeviceGraph& g_;
   int maxW_ = 1;
   DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
-      ctr_, small_, pairs_, slabF_, slabE_;
+      ctr_, small_, pairs_, slabF_, slabE_, anyvis_;
+  double filter_frac_ = 0.0;  // skip unvisited neighbours while visited edges < frac * nnz
   size_t scan_bytes_ = 0;
   std::unique_ptr<PinnedBuf> hctr_;
   int32_t epoch_ = 0;
   std::string dirs_;
-  int unroll_ = 4;
+  int unroll_ = 8;
 };
 
 template <int W, bool COUNT>
@@ -896,6 +949,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
   MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(vis_[1].p, 0, vb, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(done_.p, 0, done_.bytes, s));
+  MSBFS_HIP_CHECK(hipMemsetAsync(anyvis_.p, 0, anyvis_.bytes, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
   MSBFS_HIP_CHECK(hipMemsetAsync(small_.p, 0, small_.bytes, s));
   unsigned long long* dF = small_.as<unsigned long long>();
@@ -936,11 +990,12 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
     k_init<W, COUNT><<<grid_for(np, kBlock), kBlock, 0, s>>>(
         dpv, dpk, np, g_.rowptr, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
         acc_[ac].as<uint64_t>(), stamp_.as<int32_t>(), epoch_, fl_[fc].as<int32_t>(),
-        ctr_.as<Ctr>(), dE, alive[0]);
+        ctr_.as<Ctr>(), dE, alive[0], anyvis_.as<uint32_t>(), g_.old2new);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   HostCtr c = read_ctr(s);
   int64_t nf = c.fl2, ef = (int64_t)c.ef2;
+  int64_t ev = (int64_t)c.ev2;  // degree sum of vertices visited by any group so far
   int64_t na = n, ea = g_.nnz;  // active estimate before the first bottom-up build
   int64_t nact = 0, nactw = 0;
   bool have_active = false, fsrc_acc = true, bottom_up = false;
@@ -987,9 +1042,16 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
       const int gf = grid_for(nt_max, L::TILE, grid);
       k_td_finalize<W, COUNT><<<gf, kBlock, 0, s>>>(
           touched_.as<int32_t>(), g_.rowptr, R, O, acc_[ac ^ 1].as<uint64_t>(), alive[alv],
-          gmask, done_.as<uint32_t>(), fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), slabF(rows),
-          slabE(rows), fl_[fc].as<int32_t>(), nf, fsrc_acc ? acc_[ac].as<uint64_t>() : nullptr);
-      rows += gf;
+          gmask, done_.as<uint32_t>(), fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+          fl_[fc].as<int32_t>(), nf, fsrc_acc ? acc_[ac].as<uint64_t>() : nullptr,
+          anyvis_.as<uint32_t>());
+      MSBFS_HIP_CHECK(hipGetLastError());
+      // new frontier bits are in acc_[ac ^ 1]
+      const int gc = grid_for(nt_max, L::TILE, grid);
+      k_count_frontier<W, COUNT, false><<<gc, kBlock, 0, s>>>(
+          fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), g_.rowptr, acc_[ac ^ 1].as<uint64_t>(),
+          nullptr, slabF(rows), slabE(rows));
+      rows += gc;
       MSBFS_HIP_CHECK(hipGetLastError());
       ac ^= 1;
       fsrc_acc = true;
@@ -1014,14 +1076,14 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
             fl_[fc].as<int32_t>(), nf, acc_[ac].as<uint64_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
       }
+      const int filter = (double)ev < filter_frac_ * (double)g_.nnz ? 1 : 0;
       if (nact) {
         auto kern = unroll_ >= 8 ? k_bu_narrow<W, COUNT, 8> : k_bu_narrow<W, COUNT, 4>;
         const int gn = grid_for(nact, L::TILE, grid);
         kern<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), nact, g_.rowptr, g_.col, R, O, alive[alv],
                                    gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
-                                   fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), slabF(rows),
-                                   slabE(rows));
-        rows += gn;
+                                   fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+                                   anyvis_.as<uint32_t>(), filter);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       if (nactw) {
@@ -1030,15 +1092,22 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
         const int64_t chunks_max = nactw + ea / kChunk + 1;
         k_bu_chunks<W><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
             actw_[0].as<int32_t>(), nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
-            alive[alv], gmask, acc_[ac].as<uint64_t>());
+            alive[alv], gmask, acc_[ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter);
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(nactw, L::TILE, grid);
         k_bu_wide_finalize<W, COUNT><<<gw, kBlock, 0, s>>>(
             actw_[0].as<int32_t>(), nactw, g_.rowptr, R, O, acc_[ac].as<uint64_t>(), alive[alv],
             gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
-            ctr_.as<Ctr>(), slabF(rows), slabE(rows));
-        rows += gw;
+            ctr_.as<Ctr>(), anyvis_.as<uint32_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
+      }
+      {
+        // new frontier bits = Wb & ~R (both still in place: the swap is below)
+        const int gc = grid_for(nact + nactw, L::TILE, grid);
+        k_count_frontier<W, COUNT, true><<<gc, kBlock, 0, s>>>(
+            fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), g_.rowptr, O, R, slabF(rows), slabE(rows));
+        MSBFS_HIP_CHECK(hipGetLastError());
+        rows += gc;
       }
       std::swap(act_[0], act_[1]);
       std::swap(actw_[0], actw_[1]);
@@ -1063,14 +1132,15 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
       const auto t2 = std::chrono::steady_clock::now();
       fprintf(stderr,
               "[msbfs bp W=%d] level %u %s nf=%lld ef=%lld -> nf'=%lld ef'=%lld touched=%u "
-              "active=%lld (wide %lld) ea=%lld  %.3f ms\n",
+              "active=%lld (wide %lld) ea=%lld ev=%lld  %.3f ms\n",
               W, level, bottom_up ? "BU" : "TD", (long long)nf, (long long)ef,
               (long long)c.fl2, (long long)c.ef2, c.touched, (long long)na, (long long)nactw,
-              (long long)ea, std::chrono::duration<double, std::milli>(t2 - tl).count());
+              (long long)ea, (long long)(ev + (long long)c.ev2), std::chrono::duration<double, std::milli>(t2 - tl).count());
       tl = t2;
     }
     nf = c.fl2;
     ef = (int64_t)c.ef2;
+    ev += (int64_t)c.ev2;
     fc ^= 1;
     alv ^= 1;
     if (st) st->levels++;

@@ -36,7 +36,7 @@ __device__ __forceinline__ void wave_sum_add(unsigned long long val, unsigned lo
 
 __global__ __launch_bounds__(kBlock) void k_init(const int32_t* src, int64_t ns, int64_t n,
                                                  const int64_t* rowptr, int32_t* dist, int32_t* fl,
-                                                 Ctr* ctr) {
+                                                 Ctr* ctr, const int32_t* relabel) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t lim = (ns + stride - 1) / stride * stride;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
@@ -44,7 +44,10 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* src, int64_t ns,
     int32_t v = -1;
     if (i < ns) {
       v = src[i];
-      if (v >= 0 && v < n) app = atomicCAS(&dist[v], -1, 0) == -1;  // main.cu:49 range check
+      if (v >= 0 && v < n) {  // main.cu:49 range check
+        if (relabel) v = relabel[v];
+        app = atomicCAS(&dist[v], -1, 0) == -1;
+      }
     }
     const uint32_t pos = wave_append(app, &ctr->fl2);
     if (app) fl[pos] = v;
@@ -245,7 +248,7 @@ class DistSolver final : public Solver {
                                        hipMemcpyHostToDevice, s));
         k_init<<<grid_for(ns, kBlock), kBlock, 0, s>>>(src_.as<int32_t>(), ns, n, g_.rowptr,
                                                        dist_.as<int32_t>(), fl_[0].as<int32_t>(),
-                                                       ctr_.as<Ctr>());
+                                                       ctr_.as<Ctr>(), g_.old2new);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       Ctr c = read(s);
@@ -352,7 +355,7 @@ class SweepSolver final : public Solver {
                                        hipMemcpyHostToDevice, s));
         k_init<<<grid_for(ns, kBlock), kBlock, 0, s>>>(src_.as<int32_t>(), ns, n, g_.rowptr,
                                                        dist_.as<int32_t>(), fl_.as<int32_t>(),
-                                                       ctr_.as<Ctr>());
+                                                       ctr_.as<Ctr>(), g_.old2new);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       // level loop: one launch per level + termination flag (main.cu:61-71)

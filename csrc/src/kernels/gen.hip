@@ -96,7 +96,7 @@ __global__ __launch_bounds__(kBlock) void k_degree_stats(const int64_t* rowptr, 
 template <int CAP>
 __global__ __launch_bounds__(256) void k_sort_rows_lds(const int64_t* rowptr, int32_t* col,
                                                       const int32_t* rows, int64_t nrows) {
-  __shared__ int32_t s[CAP];
+  extern __shared__ __attribute__((aligned(16))) int32_t s[];
   for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     const int32_t v = rows[r];
     const int64_t b = rowptr[v];
@@ -123,18 +123,22 @@ __global__ __launch_bounds__(256) void k_sort_rows_lds(const int64_t* rowptr, in
 __global__ __launch_bounds__(kBlock) void k_bucket_rows(const int64_t* rowptr, int64_t n,
                                                         int32_t* small, uint32_t* nsmall,
                                                         int32_t* mid, uint32_t* nmid,
-                                                        int32_t* big, uint32_t* nbig) {
+                                                        int32_t* big, uint32_t* nbig,
+                                                        int32_t* huge, uint32_t* nhuge) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t lim = (n + stride - 1) / stride * stride;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
     const int64_t d = i < n ? rowptr[i + 1] - rowptr[i] : 0;
-    const bool a = d > 1 && d <= 64, bm = d > 64 && d <= 1024, c = d > 1024;
+    const bool a = d > 1 && d <= 64, bm = d > 64 && d <= 1024, c = d > 1024 && d <= 16384;
     const uint32_t pa = wave_append(a, nsmall);
     const uint32_t pb = wave_append(bm, nmid);
     const uint32_t pc = wave_append(c, nbig);
+    const bool h = d > 16384;
+    const uint32_t ph = wave_append(h, nhuge);
     if (a) small[pa] = (int32_t)i;
     if (bm) mid[pb] = (int32_t)i;
     if (c) big[pc] = (int32_t)i;
+    if (h) huge[ph] = (int32_t)i;
   }
 }
 
@@ -270,20 +274,107 @@ void device_graph_gen_uniform(DeviceGraph& g, int64_t n, int64_t m, uint64_t see
   device_graph_stats(g, s);
 }
 
+namespace {
+__global__ __launch_bounds__(kBlock) void k_deg_iota(const int64_t* rowptr, int64_t n,
+                                                     uint32_t* deg, int32_t* ids) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    deg[i] = (uint32_t)(rowptr[i + 1] - rowptr[i]);
+    ids[i] = (int32_t)i;
+  }
+}
+__global__ __launch_bounds__(kBlock) void k_invert_perm(const int32_t* perm, int64_t n,
+                                                        int32_t* old2new, const uint32_t* sdeg,
+                                                        int64_t* newdeg) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    old2new[perm[i]] = (int32_t)i;
+    newdeg[i] = (int64_t)sdeg[i];
+  }
+}
+// one wave per new row: copy the old row of perm[i], mapping every neighbour through old2new
+__global__ __launch_bounds__(kBlock) void k_gather_rows(const int64_t* orow, const int32_t* ocol,
+                                                        const int32_t* perm, const int64_t* nrow,
+                                                        const int32_t* old2new, int32_t* ncol,
+                                                        int64_t n) {
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int lane = lane_id();
+  for (int64_t i = wave; i < n; i += nwaves) {
+    const int32_t o = perm[i];
+    const int64_t b = orow[o], len = orow[o + 1] - b, nb = nrow[i];
+    for (int64_t j = lane; j < len; j += 64) ncol[nb + j] = old2new[ocol[b + j]];
+  }
+}
+}  // namespace
+
+void device_graph_relabel_by_degree(DeviceGraph& g, hipStream_t s) {
+  const int64_t n = g.n;
+  if (n == 0 || g.old2new) return;
+  DevBuf deg(n * 4), sdeg(n * 4), ids(n * 4), perm(n * 4), newdeg(n * 8);
+  k_deg_iota<<<grid_for(n, kBlock), kBlock, 0, s>>>(g.rowptr, n, deg.as<uint32_t>(),
+                                                    ids.as<int32_t>());
+  MSBFS_HIP_CHECK(hipGetLastError());
+  size_t tb = 0;
+  MSBFS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(
+      nullptr, tb, deg.as<uint32_t>(), sdeg.as<uint32_t>(), ids.as<int32_t>(), perm.as<int32_t>(),
+      (int)n, 0, 32, s));
+  {
+    DevBuf temp(tb);
+    MSBFS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(
+        temp.p, tb, deg.as<uint32_t>(), sdeg.as<uint32_t>(), ids.as<int32_t>(),
+        perm.as<int32_t>(), (int)n, 0, 32, s));
+  }
+  deg.release();
+  ids.release();
+  g.own_old2new.alloc(n * 4);
+  int32_t* o2n = g.own_old2new.as<int32_t>();
+  k_invert_perm<<<grid_for(n, kBlock), kBlock, 0, s>>>(perm.as<int32_t>(), n, o2n,
+                                                       sdeg.as<uint32_t>(), newdeg.as<int64_t>());
+  MSBFS_HIP_CHECK(hipGetLastError());
+  sdeg.release();
+  // new rowptr = scan of the sorted degrees
+  DevBuf nrow((n + 1) * 8);
+  MSBFS_HIP_CHECK(hipMemsetAsync(nrow.p, 0, 8, s));
+  size_t sb = 0;
+  MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, newdeg.as<int64_t>(),
+                                                   nrow.as<int64_t>() + 1, (int)n, s));
+  {
+    DevBuf temp(sb);
+    MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(temp.p, sb, newdeg.as<int64_t>(),
+                                                     nrow.as<int64_t>() + 1, (int)n, s));
+  }
+  newdeg.release();
+  DevBuf ncol((size_t)std::max<int64_t>(g.nnz, 1) * 4);
+  k_gather_rows<<<grid_for(n * 64, kBlock, 8192), kBlock, 0, s>>>(
+      g.rowptr, g.col, perm.as<int32_t>(), nrow.as<int64_t>(), o2n, ncol.as<int32_t>(), n);
+  MSBFS_HIP_CHECK(hipGetLastError());
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  g.own_rowptr = std::move(nrow);
+  g.own_col = std::move(ncol);
+  g.rowptr = g.own_rowptr.as<int64_t>();
+  g.col = g.own_col.as<int32_t>();
+  g.old2new = o2n;
+  device_graph_sort_rows(g, s);
+  device_graph_stats(g, s);
+}
+
 void device_graph_sort_rows(DeviceGraph& g, hipStream_t s) {
   // Sorted rows make the device CSR deterministic (the atomic scatter is not) and give bottom-up
   // sweeps ascending-id neighbour order. Rows > 1024 are sorted with a segmented radix sort.
   const int64_t n = g.n;
   if (n == 0) return;
-  DevBuf lists((size_t)3 * n * sizeof(int32_t)), cnts(4 * sizeof(uint32_t));
+  DevBuf lists((size_t)4 * n * sizeof(int32_t)), cnts(4 * sizeof(uint32_t));
   int32_t* small = lists.as<int32_t>();
   int32_t* mid = small + n;
   int32_t* big = mid + n;
+  int32_t* hugel = big + n;
   uint32_t* c = cnts.as<uint32_t>();
   MSBFS_HIP_CHECK(hipMemsetAsync(c, 0, cnts.bytes, s));
-  k_bucket_rows<<<grid_for(n, kBlock), kBlock, 0, s>>>(g.rowptr, n, small, c, mid, c + 1, big, c + 2);
+  k_bucket_rows<<<grid_for(n, kBlock), kBlock, 0, s>>>(g.rowptr, n, small, c, mid, c + 1, big,
+                                                       c + 2, hugel, c + 3);
   MSBFS_HIP_CHECK(hipGetLastError());
-  uint32_t h[3];
+  uint32_t h[4];
   MSBFS_HIP_CHECK(hipMemcpyAsync(h, c, sizeof(h), hipMemcpyDeviceToHost, s));
   MSBFS_HIP_CHECK(hipStreamSynchronize(s));
   if (h[0]) {
@@ -291,12 +382,18 @@ void device_graph_sort_rows(DeviceGraph& g, hipStream_t s) {
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   if (h[1]) {
-    k_sort_rows_lds<1024><<<std::min<uint32_t>(h[1], 4096), 256, 0, s>>>(g.rowptr, g.col, mid, h[1]);
+    k_sort_rows_lds<1024><<<std::min<uint32_t>(h[1], 4096), 256, 1024 * 4, s>>>(g.rowptr, g.col,
+                                                                             mid, h[1]);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   if (h[2]) {
-    std::vector<int32_t> rows(h[2]);
-    MSBFS_HIP_CHECK(hipMemcpyAsync(rows.data(), big, h[2] * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    k_sort_rows_lds<16384><<<std::min<uint32_t>(h[2], 1024), 256, 16384 * 4, s>>>(
+        g.rowptr, g.col, big, h[2]);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  if (h[3]) {
+    std::vector<int32_t> rows(h[3]);
+    MSBFS_HIP_CHECK(hipMemcpyAsync(rows.data(), hugel, h[3] * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     std::vector<int64_t> rp(n + 1);
     MSBFS_HIP_CHECK(hipMemcpyAsync(rp.data(), g.rowptr, (n + 1) * sizeof(int64_t),
                                    hipMemcpyDeviceToHost, s));

@@ -136,6 +136,9 @@ class DeviceGraph:
         self._h = handle
         self.device = device
         self._keepalive = keepalive
+        self._refresh()
+
+    def _refresh(self) -> None:
         n, nnz, m, mx, iso = (C.c_int64() for _ in range(5))
         native.check(native.lib().msbfs_graph_info(self._h, C.byref(n), C.byref(nnz), C.byref(m),
                                                    C.byref(mx), C.byref(iso)))
@@ -159,12 +162,13 @@ class DeviceGraph:
     @classmethod
     def rmat(cls, scale: int, edgefactor: int = 16, seed: int = 1, a: float = 0.57,
              b: float = 0.19, c: float = 0.19, scramble: bool = True,
-             device: int = 0) -> "DeviceGraph":
+             device: int = 0, relabel: bool = False) -> "DeviceGraph":
         """Generate the RMAT graph directly in HBM (two-pass count/scatter, no edge list)."""
         h = C.c_void_p()
         native.check(native.lib().msbfs_graph_gen_rmat(device, scale, edgefactor, seed, a, b, c,
                                                        int(scramble), C.byref(h)))
-        return cls(h, device)
+        g = cls(h, device)
+        return g.relabel_by_degree() if relabel else g
 
     @classmethod
     def uniform(cls, n: int, m: int, seed: int = 1, device: int = 0) -> "DeviceGraph":
@@ -190,6 +194,24 @@ class DeviceGraph:
     def sort_rows(self) -> "DeviceGraph":
         native.check(native.lib().msbfs_graph_sort_rows(self.handle))
         return self
+
+    def relabel_by_degree(self) -> "DeviceGraph":
+        """Renumber vertices by descending degree (hubs first, sorted rows) in place. Queries
+        keep using the original ids — solvers map sources through the stored map; F(U) is
+        label-invariant. download() then returns the relabelled CSR."""
+        native.check(native.lib().msbfs_graph_relabel_by_degree(self.handle))
+        self._refresh()
+        return self
+
+    @property
+    def relabelled(self) -> bool:
+        return bool(native.lib().msbfs_graph_is_relabelled(self.handle))
+
+    def relabel_map(self) -> np.ndarray:
+        """old2new[v] = internal id of user vertex v."""
+        out = np.empty(self.n, dtype=np.int32)
+        native.check(native.lib().msbfs_graph_relabel_map(self.handle, native.ptr(out, C.c_int32)))
+        return out
 
     def download(self) -> Graph:
         rowptr = np.empty(self.n + 1, dtype=np.int64)

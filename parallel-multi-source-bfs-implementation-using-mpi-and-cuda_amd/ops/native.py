@@ -76,6 +76,9 @@ def _sig(lib):
                                            C.c_double, C.c_double, C.c_int, P(vp)]),
         "msbfs_graph_gen_uniform": (C.c_int, [C.c_int, C.c_int64, C.c_int64, C.c_uint64, P(vp)]),
         "msbfs_graph_sort_rows": (C.c_int, [vp]),
+        "msbfs_graph_relabel_by_degree": (C.c_int, [vp]),
+        "msbfs_graph_relabel_map": (C.c_int, [vp, i32p]),
+        "msbfs_graph_is_relabelled": (C.c_int, [vp]),
         "msbfs_graph_info": (C.c_int, [vp, i64p, i64p, i64p, i64p, i64p]),
         "msbfs_graph_device_ptrs": (C.c_int, [vp, P(vp), P(vp)]),
         "msbfs_graph_download": (C.c_int, [vp, i64p, i32p]),

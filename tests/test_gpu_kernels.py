@@ -138,3 +138,27 @@ def test_bitpar_large_rmat_vs_cpu(msbfs_pkg, scale, K):
             assert np.array_equal(r.edges, ref.edges)
     with m.Solver(dg, "dist") as s:
         assert np.array_equal(s.run(qs.subset(range(8))).F, ref.F[:8])
+
+
+@pytest.mark.parametrize("algo", ["bitpar", "dist", "sweep"])
+def test_relabelled_graph_same_answers(msbfs_pkg, algo):
+    m = msbfs_pkg
+    dg = m.DeviceGraph.rmat(14, 16, 5, device=0)
+    host = dg.download()
+    qs = m.QuerySet.random(dg.n, 300 if algo == "bitpar" else 5, 6, seed=2)
+    qs = m.QuerySet.from_groups([list(g) + [-1, dg.n + 3] for g in qs.groups()])  # + invalid ids
+    ref = m.cpu_bfs(host, qs, count_edges=True)
+    dg.relabel_by_degree()
+    assert dg.relabelled
+    r = dg.download()
+    deg = np.diff(r.rowptr)
+    assert np.all(np.diff(deg) <= 0)  # degree-descending ids
+    o2n = dg.relabel_map()
+    assert np.array_equal(np.sort(o2n), np.arange(dg.n))
+    assert np.array_equal(np.diff(host.rowptr), deg[o2n])
+    for v in range(0, dg.n, 97):
+        assert np.all(np.diff(r.col[r.rowptr[v]:r.rowptr[v + 1]]) >= 0)
+    with m.Solver(dg, algo, max_groups=qs.K) as s:
+        res = s.run(qs, count_edges=True)
+    assert np.array_equal(res.F, ref.F)
+    assert np.array_equal(res.edges, ref.edges)

@@ -20,11 +20,14 @@ for s in "$@"; do
     bench20) step bench20 300 python bench.py --scale 20 --steps 3 --warmup 1 --verify 32 ;;
     bench22) step bench22 300 python bench.py --scale 22 --steps 3 --warmup 1 --verify 16 ;;
     bench26) step bench26 900 python bench.py --steps 3 --warmup 1 ;;
-    trace26) MSBFS_TRACE=1 step trace26 600 python bench.py --steps 1 --warmup 0 ;;
+    trace26) MSBFS_TRACE=1 step trace26 600 python bench.py --steps 2 --warmup 0 ;;
     prof26) export TMPDIR=/tmp; step prof26 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof26 -o run -- python bench.py --steps 1 --warmup 0 ;;
     sweep26) step sweep26 900 python bench.py --algo sweep --groups 4 --steps 1 --warmup 0 ;;
     dist26) step dist26 900 python bench.py --algo dist --groups 16 --steps 1 --warmup 0 ;;
     verify26) step verify26 900 python bench.py --steps 1 --warmup 0 --verify 64 ;;
+    filt0) MSBFS_FILTER_FRAC=0 MSBFS_TRACE=1 step filt0 600 python bench.py --steps 2 --warmup 0 ;;
+    filt2) MSBFS_FILTER_FRAC=2 MSBFS_TRACE=1 step filt2 600 python bench.py --steps 2 --warmup 0 ;;
+    unroll8) MSBFS_UNROLL=8 MSBFS_TRACE=1 step unroll8 600 python bench.py --steps 2 --warmup 0 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
