@@ -646,9 +646,15 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
   block_sum_add(ev, &ctr->ev2.v, scratch);
 }
 
-// bottom-up, wide vertices, phase 1: one wave per edge chunk (<= kChunk edges). S = 64/G
-// sub-groups stride the chunk, OR-reduce across sub-groups for the early-exit test, and merge
-// the chunk's new bits into acc[v] with atomicOr. offs = inclusive prefix of chunk counts.
+// bottom-up, wide vertices, phase 1: one wave per edge chunk (<= kChunk edges), processed in
+// tiles of 256 edges so the dependent loads are batched instead of chained per neighbour:
+//   A) all 64 lanes load 4 column ids each (one coalesced 1-KB pass), optionally test them
+//      against the visited-by-anyone bitmap (256 independent loads), and compact the survivors
+//      into an LDS list (ballot + popcount prefix);
+//   B) the S = 64/G lane groups pull 4 neighbour rows each per step (4*S rows in flight per
+//      wave), OR-reduce across groups (xor shuffles) and stop once every alive group is covered.
+// The chunk's new bits are merged into acc[v] with atomicOr (k_bu_wide_finalize folds them in).
+// offs = inclusive prefix of chunk counts over the wide list.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_bu_chunks(
     const int32_t* wl, int64_t nw, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
@@ -656,7 +662,10 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
     const uint32_t* anyvis, int filter) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
+  constexpr int T = 256;  // edges per tile
+  __shared__ int32_t tile[kWaves][T];
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  int32_t* lst = tile[threadIdx.x >> 6];
   const int64_t nchunks = offs[nw - 1];
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -682,29 +691,56 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
       lane_open |= (unv.w[j] & ~g.w[j]) != 0;
     }
     if (!__ballot(lane_open)) continue;  // wave-uniform
-    for (int64_t e0 = beg; e0 < lim; e0 += 4 * S) {
+    bool covered = false;
+    for (int64_t t0 = beg; t0 < lim && !covered; t0 += T) {
+      // ---- phase A: ids of this tile, filtered, compacted into lst[0..cnt)
       int32_t u[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t e = e0 + sub + (int64_t)q * S;
+        const int64_t e = t0 + q * 64 + lane;
         u[q] = e < lim ? col[e] : -1;
-        if (filter && u[q] >= 0 && !any_visited(anyvis, u[q])) u[q] = -1;
       }
+      if (filter) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (u[q] >= 0) {
-          const V<VW> x = ldv<VW>(R + (int64_t)u[q] * W + slot * VW);
+        for (int q = 0; q < 4; ++q)
+          if (u[q] >= 0 && !any_visited(anyvis, u[q])) u[q] = -1;
+      }
+      int cnt = 0;
 #pragma unroll
-          for (int j = 0; j < VW; ++j) a.w[j] |= x.w[j];
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t m = __ballot(u[q] >= 0);
+        if (u[q] >= 0) lst[cnt + __popcll(m & lanemask_lt())] = u[q];
+        cnt += __popcll(m);
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- phase B: rows of the surviving neighbours, 4 per lane group per step
+      for (int b = 0; b < cnt; b += 4 * S) {
+        int32_t uu[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = b + q * S + sub;
+          uu[q] = k < cnt ? lst[k] : -1;
         }
 #pragma unroll
-      for (int off = G; off < 64; off <<= 1)
+        for (int q = 0; q < 4; ++q)
+          if (uu[q] >= 0) {
+            const V<VW> x = ldv<VW>(R + (int64_t)uu[q] * W + slot * VW);
 #pragma unroll
-        for (int j = 0; j < VW; ++j) a.w[j] |= __shfl_xor(a.w[j], off);
-      bool cov = true;
+            for (int j = 0; j < VW; ++j) a.w[j] |= x.w[j];
+          }
 #pragma unroll
-      for (int j = 0; j < VW; ++j) cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
-      if (!__ballot(!cov)) break;
+        for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+          for (int j = 0; j < VW; ++j) a.w[j] |= __shfl_xor(a.w[j], off);
+        bool cov = true;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
+        if (!__ballot(!cov)) {
+          covered = true;
+          break;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // lst is rewritten by the next tile
     }
     if (sub == 0) {
 #pragma unroll
@@ -931,7 +967,7 @@ class BitparSolver final : public Solver {
   int maxW_ = 1;
   DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
       ctr_, small_, pairs_, slabF_, slabE_, anyvis_;
-  double filter_frac_ = 0.0;  // skip unvisited neighbours while visited edges < frac * nnz
+  double filter_frac_ = 0.5;  // skip unvisited neighbours while visited edges < frac * nnz
   size_t scan_bytes_ = 0;
   std::unique_ptr<PinnedBuf> hctr_;
   int32_t epoch_ = 0;
