@@ -543,13 +543,15 @@ template <int W, bool COUNT, int U>
 __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
-    int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int filter) {
+    int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int filter, int32_t* actw2,
+    int next_wide) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
-  __shared__ LdsQueue qa, qf;
+  __shared__ LdsQueue qa, qf, qw;
   __shared__ unsigned long long scratch[kWaves];
   q_init(qa);
   q_init(qf);
+  q_init(qw);
   __syncthreads();
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
   const int wv = threadIdx.x >> 6;
@@ -634,12 +636,15 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
         ev += deg;
       }
     }
-    q_push(qa, keep, v);
+    q_push(qa, keep && (int)deg <= next_wide, v);
+    q_push(qw, keep && (int)deg > next_wide, v);
     q_push(qf, app, v);
     q_flush(qa, act2, &ctr->act2.v, TILE, false);
+    q_flush(qw, actw2, &ctr->actw2.v, TILE, false);
     q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
   }
   q_flush(qa, act2, &ctr->act2.v, 0, true);
+  q_flush(qw, actw2, &ctr->actw2.v, 0, true);
   q_flush(qf, fl2, &ctr->fl2.v, 0, true);
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
@@ -663,6 +668,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
   constexpr int T = 256;  // edges per tile
+  constexpr int PB = 8;   // rows in flight per lane group in phase B
   __shared__ int32_t tile[kWaves][T];
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
   int32_t* lst = tile[threadIdx.x >> 6];
@@ -714,15 +720,15 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
       }
       __builtin_amdgcn_wave_barrier();
       // ---- phase B: rows of the surviving neighbours, 4 per lane group per step
-      for (int b = 0; b < cnt; b += 4 * S) {
-        int32_t uu[4];
+      for (int b = 0; b < cnt; b += PB * S) {
+        int32_t uu[PB];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < PB; ++q) {
           const int k = b + q * S + sub;
           uu[q] = k < cnt ? lst[k] : -1;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < PB; ++q)
           if (uu[q] >= 0) {
             const V<VW> x = ldv<VW>(R + (int64_t)uu[q] * W + slot * VW);
 #pragma unroll
@@ -757,13 +763,14 @@ template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, uint64_t* Wb,
     uint64_t* acc, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* actw2,
-    int32_t* fl2, Ctr* ctr, uint32_t* anyvis) {
+    int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* act2n, int next_wide) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
-  __shared__ LdsQueue qa, qf;
+  __shared__ LdsQueue qa, qf, qn;
   __shared__ unsigned long long scratch[kWaves];
   q_init(qa);
   q_init(qf);
+  q_init(qn);
   __syncthreads();
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
   const int wv = threadIdx.x >> 6;
@@ -812,12 +819,15 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
         ev += deg;
       }
     }
-    q_push(qa, keep, v);
+    q_push(qa, keep && (int)deg > next_wide, v);
+    q_push(qn, keep && (int)deg <= next_wide, v);
     q_push(qf, app, v);
     q_flush(qa, actw2, &ctr->actw2.v, TILE, false);
+    q_flush(qn, act2n, &ctr->act2.v, TILE, false);
     q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
   }
   q_flush(qa, actw2, &ctr->actw2.v, 0, true);
+  q_flush(qn, act2n, &ctr->act2.v, 0, true);
   q_flush(qf, fl2, &ctr->fl2.v, 0, true);
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
@@ -915,6 +925,7 @@ class BitparSolver final : public Solver {
     hctr_ = std::make_unique<PinnedBuf>(sizeof(Ctr));
     if (const char* d = getenv("MSBFS_DIRS")) dirs_ = d;  // per-level T/B override (tuning)
     if (const char* u = getenv("MSBFS_UNROLL")) unroll_ = atoi(u);
+    if (const char* w = getenv("MSBFS_WIDE_LATER")) wide_later_ = atoi(w);
     MSBFS_HIP_CHECK(hipDeviceSynchronize());
   }
 
@@ -973,6 +984,7 @@ class BitparSolver final : public Solver {
   int32_t epoch_ = 0;
   std::string dirs_;
   int unroll_ = 8;
+  int wide_later_ = 1024;
 };
 
 template <int W, bool COUNT>
@@ -1113,13 +1125,17 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       const int filter = (double)ev < filter_frac_ * (double)g_.nnz ? 1 : 0;
+      // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
+      // off only for much higher degrees, so the next lists are split at a higher threshold
+      const int next_wide = std::max(opt.wide_degree, wide_later_);
       if (nact) {
         auto kern = unroll_ >= 8 ? k_bu_narrow<W, COUNT, 8> : k_bu_narrow<W, COUNT, 4>;
         const int gn = grid_for(nact, L::TILE, grid);
         kern<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), nact, g_.rowptr, g_.col, R, O, alive[alv],
                                    gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                    fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
-                                   anyvis_.as<uint32_t>(), filter);
+                                   anyvis_.as<uint32_t>(), filter, actw_[1].as<int32_t>(),
+                                   next_wide);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       if (nactw) {
@@ -1134,7 +1150,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
         k_bu_wide_finalize<W, COUNT><<<gw, kBlock, 0, s>>>(
             actw_[0].as<int32_t>(), nactw, g_.rowptr, R, O, acc_[ac].as<uint64_t>(), alive[alv],
             gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
-            ctr_.as<Ctr>(), anyvis_.as<uint32_t>());
+            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), act_[1].as<int32_t>(), next_wide);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       {

@@ -28,6 +28,11 @@ for s in "$@"; do
     filt0) MSBFS_FILTER_FRAC=0 MSBFS_TRACE=1 step filt0 600 python bench.py --steps 2 --warmup 0 ;;
     filt2) MSBFS_FILTER_FRAC=2 MSBFS_TRACE=1 step filt2 600 python bench.py --steps 2 --warmup 0 ;;
     unroll8) MSBFS_UNROLL=8 MSBFS_TRACE=1 step unroll8 600 python bench.py --steps 2 --warmup 0 ;;
+    words8) MSBFS_TRACE=1 step words8 600 python bench.py --steps 2 --warmup 0 --max-words 8 ;;
+    wide32) MSBFS_TRACE=1 step wide32 600 python bench.py --steps 2 --warmup 0 --wide-degree 32 ;;
+    wide256) MSBFS_TRACE=1 step wide256 600 python bench.py --steps 2 --warmup 0 --wide-degree 256 ;;
+    wl128) MSBFS_WIDE_LATER=128 MSBFS_TRACE=1 step wl128 600 python bench.py --steps 2 --warmup 0 ;;
+    wl1024) MSBFS_WIDE_LATER=1024 MSBFS_TRACE=1 step wl1024 600 python bench.py --steps 2 --warmup 0 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
