@@ -1,0 +1,80 @@
+// Block-level list building for grid-stride level kernels (HIP only).
+//
+// Appending to a global list with one atomic per wave serialises on the counter's cache line
+// (device-scope atomics on one address execute one at a time at the memory side); building
+// frontiers / active lists that way cost more than the traversal itself. Here each block
+// collects items in an LDS queue (wave-aggregated LDS atomics) and flushes it with ONE global
+// atomic per ~kQCap items, writing the items out as a contiguous, coalesced run.
+#pragma once
+
+#include "msbfs/device.hpp"
+
+namespace msbfs {
+
+constexpr int kQCap = 1024;  // LDS queue capacity (items) per block
+
+struct LdsQueue {
+  int32_t item[kQCap];
+  uint32_t n;
+  uint32_t base;
+};
+
+// Call from every thread, followed by a __syncthreads() before the first push.
+__device__ __forceinline__ void q_init(LdsQueue& q) {
+  if (threadIdx.x == 0) q.n = 0;
+}
+
+// wave-aggregated push into the block queue (call from converged wave code)
+__device__ __forceinline__ void q_push(LdsQueue& q, bool pred, int32_t v) {
+  const uint64_t mask = __ballot(pred);
+  if (!mask) return;
+  const int leader = __ffsll((unsigned long long)mask) - 1;
+  uint32_t pos = 0;
+  if (lane_id() == leader) pos = atomicAdd(&q.n, (uint32_t)__popcll(mask));
+  pos = __shfl(pos, leader) + (uint32_t)__popcll(mask & lanemask_lt());
+  if (pred) q.item[pos] = v;
+}
+
+// Flush the queue to out[] when it may not hold another `room` items (or always, at the end).
+// Must be called by every thread of the block (block-uniform control flow).
+__device__ __forceinline__ void q_flush(LdsQueue& q, int32_t* out, uint32_t* gcnt, int room,
+                                        bool force) {
+  __syncthreads();
+  const uint32_t n = q.n;
+  __syncthreads();
+  if (n == 0 || (!force && n + (uint32_t)room <= (uint32_t)kQCap)) return;
+  if (threadIdx.x == 0) q.base = atomicAdd(gcnt, n);
+  __syncthreads();
+  const uint32_t base = q.base;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[base + i] = q.item[i];
+  __syncthreads();
+  if (threadIdx.x == 0) q.n = 0;
+  __syncthreads();
+}
+
+// block-wide sum of per-thread values, one atomic per block; scratch holds blockDim/64 values
+__device__ __forceinline__ void block_sum_add(unsigned long long val, unsigned long long* dst,
+                                              unsigned long long* scratch) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
+  __syncthreads();
+  if (lane_id() == 0) scratch[threadIdx.x >> 6] = val;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += scratch[w];
+    if (t) atomicAdd(dst, t);
+  }
+}
+
+// Device counters; every field on its own 128-B line so unrelated atomics never share a line.
+struct alignas(128) Slot32 {
+  uint32_t v;
+  uint32_t pad[31];
+};
+struct alignas(128) Slot64 {
+  unsigned long long v;
+  uint32_t pad[30];
+};
+
+}  // namespace msbfs

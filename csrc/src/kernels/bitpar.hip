@@ -36,13 +36,13 @@
 #include <string>
 
 #include "msbfs/device.hpp"
+#include "msbfs/device_lists.hpp"
 
 namespace msbfs {
 namespace bp {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kQCap = 1024;       // LDS queue capacity (items) per block
 constexpr int kChunk = 1024;      // bottom-up edge chunk for wide vertices
 constexpr int kMaxGrid = 2048;    // blocks of the grid-stride level kernels
 
@@ -93,15 +93,6 @@ __device__ __forceinline__ V<VW> vzero() {
   return r;
 }
 
-// Device counters; every field on its own 128-B line so unrelated atomics never share a line.
-struct alignas(128) Slot32 {
-  uint32_t v;
-  uint32_t pad[31];
-};
-struct alignas(128) Slot64 {
-  unsigned long long v;
-  uint32_t pad[30];
-};
 struct Ctr {
   Slot32 act2, actw2, fl2, touched;
   Slot64 ef2;  // sum of degrees of the next frontier
@@ -125,60 +116,6 @@ __device__ __forceinline__ void set_done(uint32_t* done, int32_t v) {
 // cleared within a batch), so pulls may skip the 8*W-byte load; a set bit only costs a load.
 __device__ __forceinline__ bool any_visited(const uint32_t* anyvis, int32_t u) {
   return (anyvis[u >> 5] >> (u & 31)) & 1u;
-}
-
-// ---- per-block LDS queues ---------------------------------------------------------------------
-struct LdsQueue {
-  int32_t item[kQCap];
-  uint32_t n;
-  uint32_t base;
-};
-
-__device__ __forceinline__ void q_init(LdsQueue& q) {
-  if (threadIdx.x == 0) q.n = 0;
-}
-
-// wave-aggregated push into the block queue (call from converged wave code)
-__device__ __forceinline__ void q_push(LdsQueue& q, bool pred, int32_t v) {
-  const uint64_t mask = __ballot(pred);
-  if (!mask) return;
-  const int leader = __ffsll((unsigned long long)mask) - 1;
-  uint32_t pos = 0;
-  if (lane_id() == leader) pos = atomicAdd(&q.n, (uint32_t)__popcll(mask));
-  pos = __shfl(pos, leader) + (uint32_t)__popcll(mask & lanemask_lt());
-  if (pred) q.item[pos] = v;
-}
-
-// Flush the queue to out[] when it may not hold another `room` items (or always, at the end).
-// Must be called by every thread of the block (block-uniform control flow).
-__device__ __forceinline__ void q_flush(LdsQueue& q, int32_t* out, uint32_t* gcnt, int room,
-                                        bool force) {
-  __syncthreads();
-  const uint32_t n = q.n;
-  __syncthreads();
-  if (n == 0 || (!force && n + (uint32_t)room <= (uint32_t)kQCap)) return;
-  if (threadIdx.x == 0) q.base = atomicAdd(gcnt, n);
-  __syncthreads();
-  const uint32_t base = q.base;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[base + i] = q.item[i];
-  __syncthreads();
-  if (threadIdx.x == 0) q.n = 0;
-  __syncthreads();
-}
-
-// block-wide sum of per-thread values, one atomic per block
-__device__ __forceinline__ void block_sum_add(unsigned long long val, unsigned long long* dst,
-                                              unsigned long long* scratch /*kWaves*/) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
-  __syncthreads();
-  if (lane_id() == 0) scratch[threadIdx.x >> 6] = val;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int w = 0; w < kWaves; ++w) t += scratch[w];
-    if (t) atomicAdd(dst, t);
-  }
 }
 
 // ---- per-group level counters in LDS ------------------------------------------------------------
@@ -687,8 +624,17 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
     const int64_t lim = min(end, beg + (int64_t)kChunk);
     const int64_t vo = (int64_t)v * W + slot * VW;
     const V<VW> r = ldv<VW>(R + vo);
-    // snapshot of bits other chunks already found (a hint; stale values only cost work)
-    const V<VW> g = ldv<VW>(acc + vo);
+    // g = bits the vertex's other chunks have published so far. Chunks of one hub run
+    // concurrently, so each tile publishes its partial OR with a RETURNING atomicOr that also
+    // hands back the current union from the memory side (atomics bypass the non-coherent per-XCD
+    // L2s); every chunk stops once the union covers all alive groups.
+    V<VW> g = vzero<VW>();
+    if (sub == 0) {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) g.w[j] = atomicOr((unsigned long long*)&acc[vo + j], 0ull);
+    }
+#pragma unroll
+    for (int j = 0; j < VW; ++j) g.w[j] = __shfl(g.w[j], slot);  // lane slot of sub-group 0
     V<VW> unv, a = vzero<VW>();
     bool lane_open = false;
 #pragma unroll
@@ -747,6 +693,23 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
         }
       }
       __builtin_amdgcn_wave_barrier();  // lst is rewritten by the next tile
+      // publish this chunk's bits so far and pick up the other chunks' (one round trip)
+      if (!covered && t0 + T < lim) {
+        bool cov = true;
+        if (sub == 0) {
+#pragma unroll
+          for (int j = 0; j < VW; ++j) {
+            const uint64_t nb = a.w[j] & unv.w[j] & ~g.w[j];
+            g.w[j] |= nb ? atomicOr((unsigned long long*)&acc[vo + j], nb)
+                         : atomicOr((unsigned long long*)&acc[vo + j], 0ull);
+            g.w[j] |= nb;
+            cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
+          }
+        }
+        if (!__ballot(!cov)) covered = true;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) g.w[j] = __shfl(g.w[j], slot);
+      }
     }
     if (sub == 0) {
 #pragma unroll

@@ -16,6 +16,7 @@
 #include <cstring>
 
 #include "msbfs/device.hpp"
+#include "msbfs/device_lists.hpp"
 
 namespace msbfs {
 namespace dist {
@@ -23,23 +24,26 @@ namespace dist {
 constexpr int kBlock = 256;
 
 struct Ctr {
-  uint32_t fl2, ul2, ulw2, pad0;
+  Slot32 fl2, ul2, ulw2, updated;
+  Slot64 ef2, eu2;
+};
+struct HostCtr {
+  uint32_t fl2, ul2, ulw2, updated;
   unsigned long long ef2, eu2;
-  uint32_t updated, pad1[3];
 };
 
-__device__ __forceinline__ void wave_sum_add(unsigned long long val, unsigned long long* dst) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
-  if (lane_id() == 0 && val) atomicAdd(dst, val);
-}
+constexpr int kWaves = kBlock / 64;
 
 __global__ __launch_bounds__(kBlock) void k_init(const int32_t* src, int64_t ns, int64_t n,
                                                  const int64_t* rowptr, int32_t* dist, int32_t* fl,
                                                  Ctr* ctr, const int32_t* relabel) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t lim = (ns + stride - 1) / stride * stride;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
+  __shared__ LdsQueue q;
+  __shared__ unsigned long long scratch[kWaves];
+  q_init(q);
+  __syncthreads();
+  unsigned long long ef = 0;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < ns; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = b + threadIdx.x;
     bool app = false;
     int32_t v = -1;
     if (i < ns) {
@@ -47,22 +51,28 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* src, int64_t ns,
       if (v >= 0 && v < n) {  // main.cu:49 range check
         if (relabel) v = relabel[v];
         app = atomicCAS(&dist[v], -1, 0) == -1;
+        if (app) ef += (unsigned long long)(rowptr[v + 1] - rowptr[v]);
       }
     }
-    const uint32_t pos = wave_append(app, &ctr->fl2);
-    if (app) fl[pos] = v;
-    wave_sum_add(app ? (unsigned long long)(rowptr[v + 1] - rowptr[v]) : 0ull, &ctr->ef2);
+    q_push(q, app, v);
+    q_flush(q, fl, &ctr->fl2.v, kBlock, false);
   }
+  q_flush(q, fl, &ctr->fl2.v, 0, true);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
 }
 
-// top-down: thread per frontier edge
+// top-down: thread per frontier edge (load-balanced search on the frontier's degree prefix)
 __global__ __launch_bounds__(kBlock) void k_td(const int32_t* fl, int64_t nf, const int64_t* offs,
                                                const int64_t* rowptr, const int32_t* col,
                                                int32_t* dist, int32_t nl, int32_t* fl2, Ctr* ctr) {
+  __shared__ LdsQueue q;
+  __shared__ unsigned long long scratch[kWaves];
+  q_init(q);
+  __syncthreads();
   const int64_t total = offs[nf - 1];
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t lim = (total + stride - 1) / stride * stride;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < lim; e += stride) {
+  unsigned long long ef = 0;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < total; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t e = b + threadIdx.x;
     bool app = false;
     int32_t v = 0;
     if (e < total) {
@@ -71,98 +81,133 @@ __global__ __launch_bounds__(kBlock) void k_td(const int32_t* fl, int64_t nf, co
       const int64_t start = i ? offs[i - 1] : 0;
       v = col[rowptr[u] + (e - start)];
       if (dist[v] < 0) app = atomicCAS(&dist[v], -1, nl) == -1;
+      if (app) ef += (unsigned long long)(rowptr[v + 1] - rowptr[v]);
     }
-    const uint32_t pos = wave_append(app, &ctr->fl2);
-    if (app) fl2[pos] = v;
-    wave_sum_add(app ? (unsigned long long)(rowptr[v + 1] - rowptr[v]) : 0ull, &ctr->ef2);
+    q_push(q, app, v);
+    q_flush(q, fl2, &ctr->fl2.v, kBlock, false);
   }
+  q_flush(q, fl2, &ctr->fl2.v, 0, true);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
 }
 
 __global__ __launch_bounds__(kBlock) void k_build_unvisited(int64_t n, const int64_t* rowptr,
                                                             const int32_t* dist, int wide,
                                                             int32_t* ul, int32_t* ulw, Ctr* ctr) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t lim = (n + stride - 1) / stride * stride;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
+  __shared__ LdsQueue qn, qw;
+  __shared__ unsigned long long scratch[kWaves];
+  q_init(qn);
+  q_init(qw);
+  __syncthreads();
+  unsigned long long eu = 0;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < n; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = b + threadIdx.x;
     int64_t d = 0;
     bool ok = false;
     if (i < n) {
       d = rowptr[i + 1] - rowptr[i];
       ok = d > 0 && dist[i] < 0;
     }
-    const bool w = ok && d > wide, nw = ok && d <= wide;
-    const uint32_t p1 = wave_append(nw, &ctr->ul2);
-    const uint32_t p2 = wave_append(w, &ctr->ulw2);
-    if (nw) ul[p1] = (int32_t)i;
-    if (w) ulw[p2] = (int32_t)i;
-    wave_sum_add(ok ? (unsigned long long)d : 0ull, &ctr->eu2);
+    if (ok) eu += (unsigned long long)d;
+    q_push(qn, ok && d <= wide, (int32_t)i);
+    q_push(qw, ok && d > wide, (int32_t)i);
+    q_flush(qn, ul, &ctr->ul2.v, kBlock, false);
+    q_flush(qw, ulw, &ctr->ulw2.v, kBlock, false);
   }
+  q_flush(qn, ul, &ctr->ul2.v, 0, true);
+  q_flush(qw, ulw, &ctr->ulw2.v, 0, true);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
 }
 
-// bottom-up, thread per unvisited narrow vertex
+// bottom-up, thread per unvisited narrow vertex: stop at the first neighbour on level L
 __global__ __launch_bounds__(kBlock) void k_bu(const int32_t* ul, int64_t nu, const int64_t* rowptr,
                                                const int32_t* col, int32_t* dist, int32_t L,
                                                int32_t* ul2, int32_t* fl2, Ctr* ctr) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t lim = (nu + stride - 1) / stride * stride;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
+  __shared__ LdsQueue qf, qk;
+  __shared__ unsigned long long scratch[kWaves];
+  q_init(qf);
+  q_init(qk);
+  __syncthreads();
+  unsigned long long ef = 0, eu = 0;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < nu; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = b + threadIdx.x;
     bool found = false, keep = false;
     int32_t v = 0;
-    unsigned long long d = 0;
     if (i < nu && dist[ul[i]] < 0) {  // visited by an intervening top-down level: drop
       v = ul[i];
-      const int64_t b = rowptr[v], e = rowptr[v + 1];
-      d = (unsigned long long)(e - b);
-      for (int64_t j = b; j < e; ++j)
+      const int64_t bb = rowptr[v], e = rowptr[v + 1];
+      for (int64_t j = bb; j < e; ++j)
         if (dist[col[j]] == L) {
           found = true;
           break;
         }
-      if (found) dist[v] = L + 1;
-      keep = !found;
+      if (found) {
+        dist[v] = L + 1;
+        ef += (unsigned long long)(e - bb);
+      } else {
+        keep = true;
+        eu += (unsigned long long)(e - bb);
+      }
     }
-    const uint32_t p1 = wave_append(found, &ctr->fl2);
-    if (found) fl2[p1] = v;
-    wave_sum_add(found ? d : 0ull, &ctr->ef2);
-    const uint32_t p2 = wave_append(keep, &ctr->ul2);
-    if (keep) ul2[p2] = v;
-    wave_sum_add(keep ? d : 0ull, &ctr->eu2);
+    q_push(qf, found, v);
+    q_push(qk, keep, v);
+    q_flush(qf, fl2, &ctr->fl2.v, kBlock, false);
+    q_flush(qk, ul2, &ctr->ul2.v, kBlock, false);
   }
+  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  q_flush(qk, ul2, &ctr->ul2.v, 0, true);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
 }
 
-// bottom-up, one wave per high-degree unvisited vertex (ballot early exit every 64 neighbours)
+// bottom-up, one wave per high-degree unvisited vertex (ballot early exit every 64 neighbours);
+// rounds are block-uniform (one vertex per wave per round) so the block queues can flush
 __global__ __launch_bounds__(kBlock) void k_bu_wide(const int32_t* ul, int64_t nu,
                                                     const int64_t* rowptr, const int32_t* col,
                                                     int32_t* dist, int32_t L, int32_t* ul2,
                                                     int32_t* fl2, Ctr* ctr) {
-  const int lane = lane_id();
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i = wave; i < nu; i += nwaves) {
-    const int32_t v = ul[i];
-    if (dist[v] >= 0) continue;  // visited by an intervening top-down level (wave-uniform)
-    const int64_t b = rowptr[v], e = rowptr[v + 1];
-    bool found = false;
-    for (int64_t j0 = b; j0 < e; j0 += 64) {
-      const int64_t j = j0 + lane;
-      const bool hit = j < e && dist[col[j]] == L;
-      if (__ballot(hit)) {
-        found = true;
-        break;
+  __shared__ LdsQueue qf, qk;
+  __shared__ unsigned long long scratch[kWaves];
+  q_init(qf);
+  q_init(qk);
+  __syncthreads();
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  unsigned long long ef = 0, eu = 0;
+  for (int64_t b = (int64_t)blockIdx.x * kWaves; b < nu; b += (int64_t)gridDim.x * kWaves) {
+    const int64_t i = b + wv;
+    bool found = false, keep = false;
+    int32_t v = 0;
+    if (i < nu) {
+      v = ul[i];
+      if (dist[v] < 0) {  // wave-uniform
+        const int64_t bb = rowptr[v], e = rowptr[v + 1];
+        for (int64_t j0 = bb; j0 < e; j0 += 64) {
+          const int64_t j = j0 + lane;
+          const bool hit = j < e && dist[col[j]] == L;
+          if (__ballot(hit)) {
+            found = true;
+            break;
+          }
+        }
+        keep = !found;
+        if (lane == 0) {
+          if (found) {
+            dist[v] = L + 1;
+            ef += (unsigned long long)(e - bb);
+          } else {
+            eu += (unsigned long long)(e - bb);
+          }
+        }
       }
     }
-    if (lane == 0) {
-      const unsigned long long d = (unsigned long long)(e - b);
-      if (found) {
-        dist[v] = L + 1;
-        fl2[atomicAdd(&ctr->fl2, 1u)] = v;
-        atomicAdd(&ctr->ef2, d);
-      } else {
-        ul2[atomicAdd(&ctr->ulw2, 1u)] = v;
-        atomicAdd(&ctr->eu2, d);
-      }
-    }
+    q_push(qf, found && lane == 0, v);
+    q_push(qk, keep && lane == 0, v);
+    q_flush(qf, fl2, &ctr->fl2.v, kWaves, false);
+    q_flush(qk, ul2, &ctr->ulw2.v, kWaves, false);
   }
+  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  q_flush(qk, ul2, &ctr->ulw2.v, 0, true);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
 }
 
 // ---- reference-algorithm sweep -------------------------------------------------------------
@@ -175,11 +220,15 @@ __global__ __launch_bounds__(kBlock) void k_sweep_level(const int64_t* rowptr, c
     if (dist[v] != L) continue;
     for (int64_t j = rowptr[v]; j < rowptr[v + 1]; ++j) {
       const int32_t u = col[j];
-      // claim with CAS instead of the reference's benign racy store (main.cu:30-33)
-      if (dist[u] == -1 && atomicCAS(&dist[u], -1, L + 1) == -1) upd = true;
+      // same benign race as the reference (main.cu:30-33): every writer stores L+1
+      if (dist[u] == -1) {
+        dist[u] = L + 1;
+        upd = true;
+      }
     }
   }
-  if (__ballot(upd) && lane_id() == 0) atomicOr(updated, 1u);
+  // one plain store per wave that found work (the reference's `*d_updated = true`)
+  if (__ballot(upd) && lane_id() == 0) *(volatile uint32_t*)updated = 1u;
 }
 
 // wave64 reduction of the distance sum (and the reached-degree sum for the TEPS numerator)
@@ -251,7 +300,7 @@ class DistSolver final : public Solver {
                                                        ctr_.as<Ctr>(), g_.old2new);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
-      Ctr c = read(s);
+      HostCtr c = read(s);
       int64_t nf = c.fl2, ef = (int64_t)c.ef2, Fk = 0, E2 = ef;
       int64_t na = n, ea = g_.nnz, nu = 0, nuw = 0;
       int fc = 0, uc = 0;
@@ -317,12 +366,11 @@ class DistSolver final : public Solver {
   }
 
  private:
-  Ctr read(hipStream_t s) {
+  HostCtr read(hipStream_t s) {
     MSBFS_HIP_CHECK(hipMemcpyAsync(hctr_->p, ctr_.p, sizeof(Ctr), hipMemcpyDeviceToHost, s));
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
-    Ctr c;
-    std::memcpy(&c, hctr_->p, sizeof(Ctr));
-    return c;
+    const Ctr* c = hctr_->as<Ctr>();
+    return HostCtr{c->fl2.v, c->ul2.v, c->ulw2.v, c->updated.v, c->ef2.v, c->eu2.v};
   }
   const DeviceGraph& g_;
   DevBuf dist_, fl_[2], ul_[2], ulw_[2], offs_, scan_tmp_, ctr_, src_;
@@ -361,16 +409,16 @@ class SweepSolver final : public Solver {
       // level loop: one launch per level + termination flag (main.cu:61-71)
       Ctr* hc = hctr_->as<Ctr>();
       for (int32_t L = 0;; ++L) {
-        MSBFS_HIP_CHECK(hipMemsetAsync(&ctr_.as<Ctr>()->updated, 0, sizeof(uint32_t), s));
+        MSBFS_HIP_CHECK(hipMemsetAsync(&ctr_.as<Ctr>()->updated.v, 0, sizeof(uint32_t), s));
         if (n)
           k_sweep_level<<<grid_for(n, kBlock, 8192), kBlock, 0, s>>>(
-              g_.rowptr, g_.col, n, dist_.as<int32_t>(), L, &ctr_.as<Ctr>()->updated);
+              g_.rowptr, g_.col, n, dist_.as<int32_t>(), L, &ctr_.as<Ctr>()->updated.v);
         MSBFS_HIP_CHECK(hipGetLastError());
-        MSBFS_HIP_CHECK(hipMemcpyAsync(&hc->updated, &ctr_.as<Ctr>()->updated, sizeof(uint32_t),
+        MSBFS_HIP_CHECK(hipMemcpyAsync(&hc->updated.v, &ctr_.as<Ctr>()->updated.v, sizeof(uint32_t),
                                        hipMemcpyDeviceToHost, s));
         MSBFS_HIP_CHECK(hipStreamSynchronize(s));
         if (st) st->levels++;
-        if (!hc->updated) break;
+        if (!hc->updated.v) break;
       }
       MSBFS_HIP_CHECK(hipMemsetAsync(red_.p, 0, red_.bytes, s));
       if (n)

@@ -33,6 +33,12 @@ for s in "$@"; do
     wide256) MSBFS_TRACE=1 step wide256 600 python bench.py --steps 2 --warmup 0 --wide-degree 256 ;;
     wl128) MSBFS_WIDE_LATER=128 MSBFS_TRACE=1 step wl128 600 python bench.py --steps 2 --warmup 0 ;;
     wl1024) MSBFS_WIDE_LATER=1024 MSBFS_TRACE=1 step wl1024 600 python bench.py --steps 2 --warmup 0 ;;
+    pmc) export TMPDIR=/tmp
+         step pmclist 120 rocprofv3 -L
+         step pmc1 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_bu|k_count" --output-format csv -d gpurun_out/pmc1 -o run -- python bench.py --steps 1 --warmup 0
+         step pmc2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_bu|k_count" --output-format csv -d gpurun_out/pmc2 -o run -- python bench.py --steps 1 --warmup 0
+         step pmc3 600 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --kernel-include-regex "k_bu|k_count" --output-format csv -d gpurun_out/pmc3 -o run -- python bench.py --steps 1 --warmup 0
+         ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
