@@ -47,6 +47,9 @@ def main() -> int:
     ap.add_argument("--beta", type=float, default=0.0)
     ap.add_argument("--wide-degree", type=int, default=0)
     ap.add_argument("--max-words", type=int, default=0)
+    ap.add_argument("--backend", default=None,
+                    help="torch.distributed backend (default nccl = RCCL); gloo lets several ranks "
+                         "share one GPU for testing")
     ap.add_argument("--relabel", type=int, default=1,
                     help="renumber vertices by descending degree after generation (preprocessing)")
     args = ap.parse_args()
@@ -56,7 +59,7 @@ def main() -> int:
     from msbfs.parallel import distributed as D
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    ctx = D.init_from_env(use_gpu=True)
+    ctx = D.init_from_env(backend=args.backend, use_gpu=True)
     dev = ctx.device
     t_setup = time.perf_counter()
     g = msbfs.DeviceGraph.rmat(args.scale, args.edgefactor, args.seed, device=dev,

@@ -480,7 +480,7 @@ template <int W, bool COUNT, int U>
 __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
-    int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int filter, int32_t* actw2,
+    int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
     int next_wide) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
@@ -522,11 +522,11 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
         int32_t u[U];
 #pragma unroll
         for (int q = 0; q < U; ++q) u[q] = (e + q < end) ? col[e + q] : -1;
-        if (filter) {
+        // ids below filter_from (degree-ordered hubs: rows hot in cache) are loaded directly;
+        // the long tail is first tested against the visited bitmap (one request either way)
 #pragma unroll
-          for (int q = 0; q < U; ++q)
-            if (u[q] >= 0 && !any_visited(anyvis, u[q])) u[q] = -1;
-        }
+        for (int q = 0; q < U; ++q)
+          if (u[q] >= filter_from && !any_visited(anyvis, u[q])) u[q] = -1;
         V<VW> x[U];
 #pragma unroll
         for (int q = 0; q < U; ++q)
@@ -601,7 +601,7 @@ template <int W>
 __global__ __launch_bounds__(kBlock) void k_bu_chunks(
     const int32_t* wl, int64_t nw, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, const uint64_t* alive, const uint64_t* gmask, uint64_t* acc,
-    const uint32_t* anyvis, int filter) {
+    const uint32_t* anyvis, int32_t filter_from, int coop) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
   constexpr int T = 256;  // edges per tile
@@ -646,20 +646,19 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
     bool covered = false;
     for (int64_t t0 = beg; t0 < lim && !covered; t0 += T) {
       // ---- phase A: ids of this tile, filtered, compacted into lst[0..cnt)
-      int32_t u[4];
+      constexpr int Q = T / 64;
+      int32_t u[Q];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < Q; ++q) {
         const int64_t e = t0 + q * 64 + lane;
         u[q] = e < lim ? col[e] : -1;
       }
-      if (filter) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (u[q] >= 0 && !any_visited(anyvis, u[q])) u[q] = -1;
-      }
+      for (int q = 0; q < Q; ++q)
+        if (u[q] >= filter_from && !any_visited(anyvis, u[q])) u[q] = -1;
       int cnt = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < Q; ++q) {
         const uint64_t m = __ballot(u[q] >= 0);
         if (u[q] >= 0) lst[cnt + __popcll(m & lanemask_lt())] = u[q];
         cnt += __popcll(m);
@@ -694,7 +693,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
       }
       __builtin_amdgcn_wave_barrier();  // lst is rewritten by the next tile
       // publish this chunk's bits so far and pick up the other chunks' (one round trip)
-      if (!covered && t0 + T < lim) {
+      if (coop && !covered && t0 + T < lim) {
         bool cov = true;
         if (sub == 0) {
 #pragma unroll
@@ -871,6 +870,7 @@ class BitparSolver final : public Solver {
     done_.alloc((size_t)((n + 31) / 32) * sizeof(uint32_t));
     anyvis_.alloc((size_t)((n + 31) / 32) * sizeof(uint32_t));
     if (const char* f = getenv("MSBFS_FILTER_FRAC")) filter_frac_ = atof(f);
+    if (const char* h = getenv("MSBFS_HUB_MB")) hub_bytes_ = atof(h) * (1 << 20);
     for (int i = 0; i < 2; ++i) {
       act_[i].alloc((size_t)n * sizeof(int32_t));
       actw_[i].alloc((size_t)n * sizeof(int32_t));
@@ -941,7 +941,8 @@ class BitparSolver final : public Solver {
   int maxW_ = 1;
   DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
       ctr_, small_, pairs_, slabF_, slabE_, anyvis_;
-  double filter_frac_ = 0.5;  // skip unvisited neighbours while visited edges < frac * nnz
+  double filter_frac_ = 0.5;
+  double hub_bytes_ = 0.0;  // MSBFS_HUB_MB: hub rows loaded without the bitmap test (measured: off is best)  // skip unvisited neighbours while visited edges < frac * nnz
   size_t scan_bytes_ = 0;
   std::unique_ptr<PinnedBuf> hctr_;
   int32_t epoch_ = 0;
@@ -1010,6 +1011,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
   int64_t na = n, ea = g_.nnz;  // active estimate before the first bottom-up build
   int64_t nact = 0, nactw = 0;
   bool have_active = false, fsrc_acc = true, bottom_up = false;
+  int st_bu_levels = 0;
   int alv = 0;
   uint32_t level = 0;
   const int grid = kMaxGrid;
@@ -1080,6 +1082,8 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
         have_active = true;
         MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
       }
+      const bool first_bu = st_bu_levels == 0;
+      ++st_bu_levels;
       if (fsrc_acc) {
         // bottom-up does not read frontier bits; clear the pending top-down ones so acc_[ac]
         // is all-zero and can collect the wide vertices' chunk results
@@ -1087,7 +1091,11 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
             fl_[fc].as<int32_t>(), nf, acc_[ac].as<uint64_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
       }
-      const int filter = (double)ev < filter_frac_ * (double)g_.nnz ? 1 : 0;
+      const bool filter = (double)ev < filter_frac_ * (double)g_.nnz;
+      // hub rows (lowest ids after degree relabelling) sized to ~hub_bytes_ are always loaded
+      const int64_t hub_ids = g_.old2new ? (int64_t)(hub_bytes_ / (8.0 * W)) : 0;
+      const int32_t filter_from =
+          filter ? (int32_t)std::min<int64_t>(hub_ids, INT32_MAX) : INT32_MAX;
       // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
       // off only for much higher degrees, so the next lists are split at a higher threshold
       const int next_wide = std::max(opt.wide_degree, wide_later_);
@@ -1097,7 +1105,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
         kern<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), nact, g_.rowptr, g_.col, R, O, alive[alv],
                                    gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                    fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
-                                   anyvis_.as<uint32_t>(), filter, actw_[1].as<int32_t>(),
+                                   anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
                                    next_wide);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
@@ -1107,7 +1115,8 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
         const int64_t chunks_max = nactw + ea / kChunk + 1;
         k_bu_chunks<W><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
             actw_[0].as<int32_t>(), nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
-            alive[alv], gmask, acc_[ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter);
+            alive[alv], gmask, acc_[ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
+            first_bu ? 0 : 1);
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(nactw, L::TILE, grid);
         k_bu_wide_finalize<W, COUNT><<<gw, kBlock, 0, s>>>(

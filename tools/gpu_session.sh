@@ -39,6 +39,22 @@ for s in "$@"; do
          step pmc2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_bu|k_count" --output-format csv -d gpurun_out/pmc2 -o run -- python bench.py --steps 1 --warmup 0
          step pmc3 600 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --kernel-include-regex "k_bu|k_count" --output-format csv -d gpurun_out/pmc3 -o run -- python bench.py --steps 1 --warmup 0
          ;;
+    g512) MSBFS_TRACE=1 step g512 600 python bench.py --steps 3 --warmup 1 --groups 512 ;;
+    g256) MSBFS_TRACE=1 step g256 600 python bench.py --steps 3 --warmup 1 --groups 256 ;;
+    g128) MSBFS_TRACE=1 step g128 600 python bench.py --steps 3 --warmup 1 --groups 128 ;;
+    g64) MSBFS_TRACE=1 step g64 600 python bench.py --steps 3 --warmup 1 --groups 64 ;;
+    g128f0) MSBFS_FILTER_FRAC=0 MSBFS_TRACE=1 step g128f0 600 python bench.py --steps 3 --warmup 1 --groups 128 ;;
+    prof128) export TMPDIR=/tmp; step prof128 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof128 -o run -- python bench.py --steps 1 --warmup 0 --groups 128 ;;
+    pmc128) export TMPDIR=/tmp
+         step pmc4 600 rocprofv3 --pmc TCC_REQ_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum --kernel-include-regex "k_bu" --output-format csv -d gpurun_out/pmc4 -o run -- python bench.py --steps 1 --warmup 0 --groups 128
+         step pmc5 600 rocprofv3 --pmc TA_BUSY_avr TCC_BUSY_avr GRBM_GUI_ACTIVE TA_ADDR_STALLED_BY_TC_CYCLES_sum --kernel-include-regex "k_bu" --output-format csv -d gpurun_out/pmc5 -o run -- python bench.py --steps 1 --warmup 0 --groups 128
+         ;;
+    hub0) MSBFS_HUB_MB=0 MSBFS_TRACE=1 step hub0 600 python bench.py --steps 3 --warmup 1 ;;
+    hub64) MSBFS_HUB_MB=64 MSBFS_TRACE=1 step hub64 600 python bench.py --steps 3 --warmup 1 ;;
+    hub128g) MSBFS_HUB_MB=64 MSBFS_TRACE=1 step hub128g 600 python bench.py --steps 3 --warmup 1 --groups 128 ;;
+    hub4g) MSBFS_HUB_MB=4 MSBFS_TRACE=1 step hub4g 600 python bench.py --steps 3 --warmup 1 --groups 128 ;;
+    mr2) step mr2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --scale 22 --steps 2 --warmup 1 --backend gloo ;;
+    mr1) step mr1 600 python bench.py --scale 22 --steps 2 --warmup 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV output (kernel trace and/or counter collection) as markdown.
+
+    python tools/prof_summary.py gpurun_out/prof26 > profiles/rmat26_kernels.md
+
+For a kernel trace it prints the per-kernel totals and the per-dispatch timeline of the LAST
+solver run in the trace (the timed step); for counter collections it prints one row per
+dispatch with every collected counter.
+"""
+import collections
+import csv
+import os
+import sys
+
+
+def load(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def short(name: str) -> str:
+    n = name.split("(")[0]
+    for p in ("void ", "msbfs::bp::", "msbfs::dist::", "msbfs::(anonymous namespace)::",
+              "msbfs::"):
+        n = n.replace(p, "")
+    return n[:48]
+
+
+def trace_summary(d):
+    p = os.path.join(d, "run_kernel_trace.csv")
+    if not os.path.exists(p):
+        return
+    rows = load(p)
+    tot = collections.defaultdict(lambda: [0, 0.0])
+    for r in rows:
+        k = short(r["Kernel_Name"])
+        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        tot[k][0] += 1
+        tot[k][1] += dur
+    print(f"### Kernel totals ({d})\n")
+    print("| kernel | calls | total ms |")
+    print("|---|---|---|")
+    for k, (c, ms) in sorted(tot.items(), key=lambda x: -x[1][1])[:25]:
+        print(f"| `{k}` | {c} | {ms:.3f} |")
+    # timeline of the last solver run: from the last init kernel on
+    starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]).startswith("k_init")]
+    if starts:
+        print(f"\n### Timeline of the last solver run\n")
+        print("| # | kernel | grid | VGPR | LDS B | ms |")
+        print("|---|---|---|---|---|---|")
+        for i, r in enumerate(rows[starts[-1]:]):
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            if dur < 0.01:
+                continue
+            print(f"| {i} | `{short(r['Kernel_Name'])}` | {r.get('Grid_Size_X', r.get('Grid_Size', ''))} | "
+                  f"{r.get('VGPR_Count', '')} | {r.get('LDS_Block_Size', '')} | {dur:.3f} |")
+    print()
+
+
+def counter_summary(d):
+    p = os.path.join(d, "run_counter_collection.csv")
+    if not os.path.exists(p):
+        return
+    rows = load(p)
+    agg = collections.OrderedDict()
+    names = []
+    for r in rows:
+        key = r["Dispatch_Id"]
+        e = agg.setdefault(key, {"kernel": short(r["Kernel_Name"]),
+                                 "ms": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6})
+        e[r["Counter_Name"]] = float(r["Counter_Value"])
+        if r["Counter_Name"] not in names:
+            names.append(r["Counter_Name"])
+    print(f"### Counters ({d}) — dispatches of the last run, > 0.2 ms\n")
+    print("| kernel | ms | " + " | ".join(names) + " |")
+    print("|---|---|" + "---|" * len(names))
+    items = list(agg.values())
+    for e in items[len(items) // 2:]:
+        if e["ms"] < 0.2:
+            continue
+        vals = " | ".join(f"{e.get(n, 0):.4g}" for n in names)
+        print(f"| `{e['kernel']}` | {e['ms']:.3f} | {vals} |")
+    print()
+
+
+if __name__ == "__main__":
+    for d in sys.argv[1:]:
+        trace_summary(d)
+        counter_summary(d)
