@@ -857,8 +857,19 @@ class BitparSolver final : public Solver {
   BitparSolver(const DeviceGraph& g, int max_groups) : g_(g) {
     int w = 1;
     while (w * 64 < max_groups && w < 16) w <<= 1;
-    maxW_ = w;
     const int64_t n = std::max<int64_t>(g.n, 1);
+    // Size the batch width to free HBM: 4 visited/accumulator buffers of n*W words plus ~48 B
+    // per vertex of lists; groups beyond 64*W run as further batches.
+    {
+      size_t free_b = 0, total_b = 0;
+      if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+        const double fixed = 48.0 * (double)n + 64.0 * (1 << 20);
+        while (w > 1 && fixed + 32.0 * (double)n * w > 0.92 * (double)free_b) w >>= 1;
+        if (fixed + 32.0 * (double)n * w > 0.92 * (double)free_b)
+          fail("not enough device memory for the bit-parallel solver (n=" + std::to_string(n) + ")");
+      }
+    }
+    maxW_ = w;
     const size_t vb = (size_t)n * maxW_ * sizeof(uint64_t);
     for (int i = 0; i < 2; ++i) {
       vis_[i].alloc(vb);

@@ -311,6 +311,14 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(const int64_t* orow, con
 void device_graph_relabel_by_degree(DeviceGraph& g, hipStream_t s) {
   const int64_t n = g.n;
   if (n == 0 || g.old2new) return;
+  {
+    // the rebuild holds a second column array next to the first
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+        (double)free_b < 1.05 * ((double)g.nnz * 4.0 + (double)n * 40.0))
+      fail("not enough device memory to relabel the graph (needs a second " +
+           std::to_string(g.nnz * 4 >> 20) + " MiB column array)");
+  }
   DevBuf deg(n * 4), sdeg(n * 4), ids(n * 4), perm(n * 4), newdeg(n * 8);
   k_deg_iota<<<grid_for(n, kBlock), kBlock, 0, s>>>(g.rowptr, n, deg.as<uint32_t>(),
                                                     ids.as<int32_t>());
