@@ -44,7 +44,7 @@ for s in "$@"; do
     g128) MSBFS_TRACE=1 step g128 600 python bench.py --steps 3 --warmup 1 --groups 128 ;;
     g64) MSBFS_TRACE=1 step g64 600 python bench.py --steps 3 --warmup 1 --groups 64 ;;
     g128f0) MSBFS_FILTER_FRAC=0 MSBFS_TRACE=1 step g128f0 600 python bench.py --steps 3 --warmup 1 --groups 128 ;;
-    prof128) export TMPDIR=/tmp; step prof128 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof128 -o run -- python bench.py --steps 1 --warmup 0 --groups 128 ;;
+    prof128) export TMPDIR=/tmp; rm -rf gpurun_out/prof128; step prof128 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof128 -o run -- python bench.py --steps 1 --warmup 0 --groups 128 ;;
     pmc128) export TMPDIR=/tmp
          step pmc4 600 rocprofv3 --pmc TCC_REQ_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum --kernel-include-regex "k_bu" --output-format csv -d gpurun_out/pmc4 -o run -- python bench.py --steps 1 --warmup 0 --groups 128
          step pmc5 600 rocprofv3 --pmc TA_BUSY_avr TCC_BUSY_avr GRBM_GUI_ACTIVE TA_ADDR_STALLED_BY_TC_CYCLES_sum --kernel-include-regex "k_bu" --output-format csv -d gpurun_out/pmc5 -o run -- python bench.py --steps 1 --warmup 0 --groups 128
@@ -55,6 +55,18 @@ for s in "$@"; do
     hub4g) MSBFS_HUB_MB=4 MSBFS_TRACE=1 step hub4g 600 python bench.py --steps 3 --warmup 1 --groups 128 ;;
     mr2) step mr2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --scale 22 --steps 2 --warmup 1 --backend gloo ;;
     mr1) step mr1 600 python bench.py --scale 22 --steps 2 --warmup 1 ;;
+    road) step road_bp 600 python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 256 --verify 4
+          step road_dist 600 python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 8 --algo dist --steps 1 ;;
+    profroad) export TMPDIR=/tmp; step profroad 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profroad -o run -- python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 256 --steps 1 ;;
+    dirs128) MSBFS_DIRS=TTBBBBBB MSBFS_TRACE=1 step d128_ttb 600 python bench.py --steps 3 --warmup 1 --groups 128
+             MSBFS_DIRS=TTTBBBBB MSBFS_TRACE=1 step d128_tttb 600 python bench.py --steps 3 --warmup 1 --groups 128
+             MSBFS_TRACE=1 step d128_auto 600 python bench.py --steps 3 --warmup 1 --groups 128
+             MSBFS_DIRS=TTBBBBBB MSBFS_TRACE=1 step d1024_ttb 600 python bench.py --steps 3 --warmup 1 ;;
+    road2) step road_td 600 python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 256 --force-dir 1
+           step road_a2 600 python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 256 --alpha 2
+           step road_1024 600 python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 1024 --force-dir 1
+           step rmat_a4 600 python tools/bench_graph.py --graph rmat:24:16 --groups 1024 --alpha 4 --relabel 1
+           step rmat_a14 600 python tools/bench_graph.py --graph rmat:24:16 --groups 1024 --relabel 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

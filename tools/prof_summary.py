@@ -13,6 +13,9 @@ import os
 import sys
 
 
+MAX_TIMELINE = 80
+
+
 def load(path):
     with open(path) as f:
         return list(csv.DictReader(f))
@@ -45,13 +48,24 @@ def trace_summary(d):
     # timeline of the last solver run: from the last init kernel on
     starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]).startswith("k_init")]
     if starts:
+        run = rows[starts[-1]:]
+        t0 = int(run[0]["Start_Timestamp"])
+        t1 = max(int(r["End_Timestamp"]) for r in run)
+        busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in run)
         print(f"\n### Timeline of the last solver run\n")
+        print(f"{len(run)} dispatches, wall (first start to last end, under the profiler) "
+              f"{(t1 - t0) / 1e6:.3f} ms, kernel busy {busy / 1e6:.3f} ms\n")
         print("| # | kernel | grid | VGPR | LDS B | ms |")
         print("|---|---|---|---|---|---|")
+        shown = 0
         for i, r in enumerate(rows[starts[-1]:]):
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
             if dur < 0.01:
                 continue
+            shown += 1
+            if shown > MAX_TIMELINE:
+                print(f"| … | (timeline truncated at {MAX_TIMELINE} dispatches) | | | | |")
+                break
             print(f"| {i} | `{short(r['Kernel_Name'])}` | {r.get('Grid_Size_X', r.get('Grid_Size', ''))} | "
                   f"{r.get('VGPR_Count', '')} | {r.get('LDS_Block_Size', '')} | {dur:.3f} |")
     print()
