@@ -50,6 +50,10 @@ def main() -> int:
     ap.add_argument("--backend", default=None,
                     help="torch.distributed backend (default nccl = RCCL); gloo lets several ranks "
                          "share one GPU for testing")
+    ap.add_argument("--dist", default="auto", choices=["auto", "roundrobin", "hybrid"],
+                    help="multi-GPU decomposition: round-robin query groups (main.cu:304-307) or "
+                         "hybrid (levels 1-2 vertex-partitioned, then query-partitioned); auto = "
+                         "hybrid when N > 1 and the groups fit one bit-parallel pass")
     ap.add_argument("--relabel", type=int, default=1,
                     help="renumber vertices by descending degree after generation (preprocessing)")
     args = ap.parse_args()
@@ -57,6 +61,7 @@ def main() -> int:
     import torch
     import msbfs
     from msbfs.parallel import distributed as D
+    from msbfs.parallel import hybrid as H
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     ctx = D.init_from_env(backend=args.backend, use_gpu=True)
@@ -71,16 +76,35 @@ def main() -> int:
         except msbfs.native.MsbfsError as e:  # e.g. RMAT-30: no room for a second col array
             print(f"bench: relabel skipped: {e}", file=sys.stderr)
     qs = msbfs.QuerySet.random(g.n, args.groups, args.group_size, args.qseed)
-    local_idx = D.round_robin(qs.K, ctx.rank, ctx.world)
+    solver = msbfs.Solver(g, args.algo, max_groups=qs.K, alpha=args.alpha, beta=args.beta,
+                          wide_degree=args.wide_degree, max_words=args.max_words)
+    mode = args.dist
+    if mode == "auto":
+        mode = ("hybrid" if ctx.world > 1 and args.algo == "bitpar"
+                and qs.K <= solver.hybrid_max_groups() else "roundrobin")
+    if mode == "hybrid":
+        runner = H.HybridRunner(solver, qs.K, ctx)
+        local_idx = runner.idx
+    else:
+        local_idx = D.round_robin(qs.K, ctx.rank, ctx.world)
     local_q = qs.subset(local_idx)
-    solver = msbfs.Solver(g, args.algo, max_groups=max(1, local_q.K), alpha=args.alpha,
-                          beta=args.beta, wide_degree=args.wide_degree, max_words=args.max_words)
     torch.cuda.synchronize(dev)
     setup_s = time.perf_counter() - t_setup
+
+    def step():
+        if mode == "hybrid":
+            res = runner.run(qs)
+            return res.F, res.stats
+        r = solver.run(local_q)
+        return r.F, r.stats
 
     # untimed: TEPS numerator (traversed edges per group) — also the first warm-up pass
     r0 = solver.run(local_q, count_edges=True)
     total_edges = int(D.allreduce_sum_i64(np.array([int(r0.edges.sum())], np.int64), ctx)[0])
+    F0, _ = step()
+    if not np.array_equal(F0, r0.F):
+        print(f"rank {ctx.rank}: {mode} F differs from the single-GPU pass", file=sys.stderr)
+        return 3
     if args.verify and ctx.rank == 0:
         nv = min(args.verify, local_q.K)
         with msbfs.Solver(g, "dist") as ds:
@@ -89,17 +113,16 @@ def main() -> int:
             print(f"VERIFY FAILED: bitpar {r0.F[:nv]} vs dist {rv.F}", file=sys.stderr)
             return 3
     for _ in range(max(0, args.warmup)):
-        r = solver.run(local_q)
-        D.packed_argmin(r.F, local_idx, qs.K, ctx)
+        F, _ = step()
+        D.packed_argmin(F, local_idx, qs.K, ctx)
 
     D.barrier(ctx)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     stats = {}
     for _ in range(args.steps):
-        r = solver.run(local_q)
-        min_k, min_f = D.packed_argmin(r.F, local_idx, qs.K, ctx)
-        stats = r.stats
+        F, stats = step()
+        min_k, min_f = D.packed_argmin(F, local_idx, qs.K, ctx)
     torch.cuda.synchronize(dev)
     D.barrier(ctx)
     dt = time.perf_counter() - t0
@@ -124,7 +147,8 @@ def main() -> int:
                 "model": f"rmat{args.scale}-ef{args.edgefactor}",
                 "global_batch": qs.K,
                 "seq_len": args.group_size,
-                "parallelism": f"dp{ctx.world}",
+                "parallelism": (f"hybrid{ctx.world} (levels 1-2 vertex-partitioned, then "
+                                f"query-partitioned)" if mode == "hybrid" else f"dp{ctx.world}"),
                 "algo": args.algo,
                 "n": g.n, "m": g.m,
                 "traversed_edges": total_edges,

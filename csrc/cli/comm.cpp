@@ -33,6 +33,20 @@ void Comm::bcast_device(void* dptr, size_t bytes, int root, hipStream_t s) {
   }
 }
 
+void Comm::alltoallv_device_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                                uint64_t* recv, const std::vector<int64_t>& rcount,
+                                hipStream_t s) {
+  int64_t ns = 0, nr = 0;
+  for (int64_t c : scount) ns += c;
+  for (int64_t c : rcount) nr += c;
+  std::vector<uint64_t> hs(std::max<int64_t>(ns, 1)), hr(std::max<int64_t>(nr, 1));
+  if (ns) MSBFS_HIP_CHECK(hipMemcpyAsync(hs.data(), send, ns * 8, hipMemcpyDeviceToHost, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  alltoallv_host_u64(hs.data(), scount, hr.data(), rcount);
+  if (nr) MSBFS_HIP_CHECK(hipMemcpyAsync(recv, hr.data(), nr * 8, hipMemcpyHostToDevice, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+}
+
 namespace {
 
 class LocalComm final : public Comm {
@@ -46,6 +60,16 @@ class LocalComm final : public Comm {
   void allreduce_sum_i64(int64_t*, size_t) override {}
   double allreduce_max_f64(double x) override { return x; }
   void allgather_u64(uint64_t x, std::vector<uint64_t>& out) override { out.assign(1, x); }
+  void alltoallv_host_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                          uint64_t* recv, const std::vector<int64_t>&) override {
+    if (scount[0]) std::memcpy(recv, send, scount[0] * 8);
+  }
+  void alltoallv_device_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                            uint64_t* recv, const std::vector<int64_t>&, hipStream_t s) override {
+    if (scount[0])
+      MSBFS_HIP_CHECK(hipMemcpyAsync(recv, send, scount[0] * 8, hipMemcpyDeviceToDevice, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  }
   [[noreturn]] void abort(int code) override { std::exit(code); }
 };
 
@@ -88,6 +112,29 @@ class MpiComm : public Comm {
   void allgather_u64(uint64_t x, std::vector<uint64_t>& out) override {
     out.resize(size_);
     MPI_Allgather(&x, 1, MPI_UINT64_T, out.data(), 1, MPI_UINT64_T, MPI_COMM_WORLD);
+  }
+  void alltoallv_host_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                          uint64_t* recv, const std::vector<int64_t>& rcount) override {
+    // MPI counts are int: every peer block travels as <= 1 GiB pieces; both sides derive the
+    // same piece count from the same block size, so nonblocking pieces pair up exactly
+    std::vector<MPI_Request> req;
+    const int64_t piece = (int64_t)(kChunk / 8);
+    int64_t so = 0, ro = 0;
+    for (int j = 0; j < size_; ++j) {
+      for (int64_t o = 0; o < rcount[j]; o += piece) {
+        req.emplace_back();
+        MPI_Irecv(recv + ro + o, (int)std::min(piece, rcount[j] - o), MPI_UINT64_T, j, 7,
+                  MPI_COMM_WORLD, &req.back());
+      }
+      for (int64_t o = 0; o < scount[j]; o += piece) {
+        req.emplace_back();
+        MPI_Isend(send + so + o, (int)std::min(piece, scount[j] - o), MPI_UINT64_T, j, 7,
+                  MPI_COMM_WORLD, &req.back());
+      }
+      so += scount[j];
+      ro += rcount[j];
+    }
+    if (!req.empty()) MPI_Waitall((int)req.size(), req.data(), MPI_STATUSES_IGNORE);
   }
   [[noreturn]] void abort(int code) override {
     // unlike main.cu:98,140 (exit without MPI_Abort -> peers hang in MPI_Bcast), take the job down
@@ -158,6 +205,26 @@ class RcclComm final : public Comm {
   double allreduce_max_f64(double x) override { return host_->allreduce_max_f64(x); }
   void allgather_u64(uint64_t x, std::vector<uint64_t>& out) override {
     host_->allgather_u64(x, out);
+  }
+  void alltoallv_host_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                          uint64_t* recv, const std::vector<int64_t>& rcount) override {
+    host_->alltoallv_host_u64(send, scount, recv, rcount);
+  }
+  void alltoallv_device_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                            uint64_t* recv, const std::vector<int64_t>& rcount,
+                            hipStream_t s) override {
+    // one grouped point-to-point round: every pair of GPUs talks over its own xGMI link at once
+    const int P = size();
+    int64_t so = 0, ro = 0;
+    NCCL_CHECK(ncclGroupStart());
+    for (int j = 0; j < P; ++j) {
+      if (scount[j]) NCCL_CHECK(ncclSend(send + so, (size_t)scount[j], ncclUint64, j, comm_, s));
+      if (rcount[j]) NCCL_CHECK(ncclRecv(recv + ro, (size_t)rcount[j], ncclUint64, j, comm_, s));
+      so += scount[j];
+      ro += rcount[j];
+    }
+    NCCL_CHECK(ncclGroupEnd());
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
   }
   [[noreturn]] void abort(int code) override {
     if (comm_) ncclCommAbort(comm_);

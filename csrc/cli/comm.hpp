@@ -35,6 +35,14 @@ class Comm {
   virtual void allreduce_sum_i64(int64_t* p, size_t n) = 0;
   virtual double allreduce_max_f64(double x) = 0;
   virtual void allgather_u64(uint64_t x, std::vector<uint64_t>& out) = 0;
+  // all-to-all of 64-bit words between device buffers (hybrid mode's visited-word exchange):
+  // scount[j] words go from send (destination-major) to rank j, rcount[r] words arrive from
+  // rank r (source-major). Default: stage through host memory + alltoallv_host.
+  virtual void alltoallv_device_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                                    uint64_t* recv, const std::vector<int64_t>& rcount,
+                                    hipStream_t s);
+  virtual void alltoallv_host_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                                  uint64_t* recv, const std::vector<int64_t>& rcount) = 0;
   [[noreturn]] virtual void abort(int code) = 0;
   virtual bool device_collectives() const { return false; }
 };

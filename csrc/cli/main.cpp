@@ -10,6 +10,8 @@
 //   --gen rmat:SCALE:EF:SEED | uniform:N:M:SEED   (per-rank device generation, no broadcast)
 //   --qgen K:SIZE:SEED                            (generated query groups)
 //   --threads N (cpu algo)  --no-cache  --json  --sort-rows  --repeat R
+//   --dist {auto,roundrobin,hybrid}  multi-rank decomposition (auto: hybrid when > 1 rank, the
+//          bit-parallel solver and K <= one pass; see kernels/bitpar.hip "hybrid")
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -32,7 +34,7 @@ using clk = std::chrono::high_resolution_clock;
 namespace {
 
 struct Args {
-  std::string graph, query, algo = "auto", comm = "auto", gen, qgen;
+  std::string graph, query, algo = "auto", comm = "auto", gen, qgen, dist = "auto";
   int numGPU = 1;
   int threads = 0;
   int repeat = 1;
@@ -79,6 +81,7 @@ int main(int argc, char* argv[]) {
     else if (!strcmp(argv[i], "-gn") && has) a.numGPU = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--algo") && has) a.algo = argv[++i];
     else if (!strcmp(argv[i], "--comm") && has) a.comm = argv[++i];
+    else if (!strcmp(argv[i], "--dist") && has) a.dist = argv[++i];
     else if (!strcmp(argv[i], "--gen") && has) a.gen = argv[++i];
     else if (!strcmp(argv[i], "--qgen") && has) a.qgen = argv[++i];
     else if (!strcmp(argv[i], "--threads") && has) a.threads = atoi(argv[++i]);
@@ -223,21 +226,20 @@ int main(int argc, char* argv[]) {
     }
     const int64_t K = q.K();
 
-    // ---- static round-robin assignment (main.cu:304-307) -------------------------------------
-    QuerySet local;
-    std::vector<int64_t> local_to_global;
-    for (int64_t k = comm->rank(); k < K; k += comm->size()) {
-      local_to_global.push_back(k);
-      local.ids.insert(local.ids.end(), q.ids.begin() + q.off[k], q.ids.begin() + q.off[k + 1]);
-      local.off.push_back((int64_t)local.ids.size());
-    }
-    const int64_t nlocal = (int64_t)local_to_global.size();
+    if (a.dist != "auto" && a.dist != "roundrobin" && a.dist != "hybrid")
+      fail("unknown --dist " + a.dist);
+    const int P = comm->size(), me = comm->rank();
+    int dalgo = algo;
+    if (!cpu && dalgo == 0) dalgo = (K + P - 1) / P > 1 || (a.dist == "hybrid" && K > 1) ? 1 : 2;
+    const bool want_hybrid =
+        !cpu && dalgo == 1 && (a.dist == "hybrid" || (a.dist == "auto" && P > 1));
 
     std::unique_ptr<Solver> solver;
     if (!cpu) {
-      int dalgo = algo;
-      if (dalgo == 0) dalgo = nlocal > 1 ? 1 : 2;
-      if (dalgo == 1) solver = make_bitpar_solver(dg, (int)std::min<int64_t>(std::max<int64_t>(nlocal, 1), 1024));
+      const int64_t rr_local = (K + P - 1) / P;
+      if (dalgo == 1)
+        solver = make_bitpar_solver(
+            dg, (int)std::min<int64_t>(std::max<int64_t>(want_hybrid ? K : rr_local, 1), 1024));
       else if (dalgo == 4) solver = make_sweep_solver(dg);
       else {
         solver = make_dist_solver(dg);
@@ -245,6 +247,53 @@ int main(int argc, char* argv[]) {
       }
       if (a.json) solver->opt.count_edges = true;
       MSBFS_HIP_CHECK(hipDeviceSynchronize());
+    }
+    const bool hybrid = want_hybrid && K >= 1 && K <= solver->hybrid_max_groups();
+    if (a.dist == "hybrid" && !hybrid && me == 0)
+      fprintf(stderr, "msbfs: --dist hybrid needs --algo bitpar and K <= %lld; using round-robin\n",
+              (long long)(solver ? solver->hybrid_max_groups() : 0));
+
+    // ---- assignment: static round-robin (main.cu:304-307), or whole 64-group words (hybrid)
+    std::vector<int32_t> wbeg(P + 1, 0);
+    std::vector<int64_t> bounds(P + 1, 0);
+    if (hybrid) {
+      const int wt = (int)((K + 63) / 64);
+      for (int j = 0; j <= P; ++j) wbeg[j] = (int32_t)((int64_t)j * wt / P);
+      hybrid_split(dg, P, 8, bounds.data());
+    }
+    QuerySet local;
+    std::vector<int64_t> local_to_global;
+    auto take = [&](int64_t k) {
+      local_to_global.push_back(k);
+      local.ids.insert(local.ids.end(), q.ids.begin() + q.off[k], q.ids.begin() + q.off[k + 1]);
+      local.off.push_back((int64_t)local.ids.size());
+    };
+    if (hybrid) {
+      for (int64_t k = 64 * (int64_t)wbeg[me]; k < std::min<int64_t>(K, 64 * (int64_t)wbeg[me + 1]);
+           ++k)
+        take(k);
+    } else {
+      for (int64_t k = me; k < K; k += P) take(k);
+    }
+    const int64_t nlocal = (int64_t)local_to_global.size();
+    // hybrid exchange buffers: send = own range x all words (destination-major), recv = all
+    // vertices x own words
+    DevBuf hsend, hrecv;
+    std::vector<int64_t> scount(P, 0), rcount(P, 0), hout, hF;
+    const int nw_me = hybrid ? wbeg[me + 1] - wbeg[me] : 0;
+    if (hybrid) {
+      const int64_t cnt = bounds[me + 1] - bounds[me];
+      int64_t ns = 0, nr = 0;
+      for (int j = 0; j < P; ++j) {
+        scount[j] = cnt * (wbeg[j + 1] - wbeg[j]);
+        rcount[j] = (bounds[j + 1] - bounds[j]) * nw_me;
+        ns += scount[j];
+        nr += rcount[j];
+      }
+      hsend.alloc((size_t)std::max<int64_t>(ns, 1) * 8);
+      hrecv.alloc((size_t)std::max<int64_t>(nr, 1) * 8);
+      hout.resize(2 * K + 3);
+      hF.resize((size_t)std::max(1, 64 * nw_me));
     }
 
     const auto t_pre1 = clk::now();  // main.cu:297-298
@@ -255,6 +304,10 @@ int main(int argc, char* argv[]) {
     double computation_time = 0;
     int64_t minF = -1, minK = -1;
     RunStats rs;
+    if (hybrid && a.json && nlocal) {  // TEPS numerator: untimed counting pass of the own groups
+      std::vector<int64_t> Ft(nlocal);
+      solver->run(nlocal, local.off.data(), local.ids.data(), Ft.data(), E2.data(), nullptr, stream);
+    }
     for (int rep = 0; rep < a.repeat; ++rep) {
       comm->barrier();
       const auto t_c0 = clk::now();
@@ -264,6 +317,17 @@ int main(int argc, char* argv[]) {
         cpu_msbfs_all(g, local, F, a.json ? &e : nullptr, a.threads > 0 ? a.threads : default_threads());
         if (a.json)
           for (int64_t i = 0; i < nlocal; ++i) E2[i] = 2 * e[i];
+      } else if (hybrid) {
+        // levels 1-2 vertex-partitioned (all groups), one word all-to-all, the rest per rank
+        rs = RunStats();
+        solver->hybrid_phase_a(K, q.off.data(), q.ids.data(), bounds[me], bounds[me + 1], me == 0,
+                               P, wbeg.data(), hsend.as<uint64_t>(), hout.data(), &rs, stream);
+        comm->alltoallv_device_u64(hsend.as<uint64_t>(), scount, hrecv.as<uint64_t>(), rcount,
+                                   stream);
+        comm->allreduce_sum_i64(hout.data(), hout.size());
+        solver->hybrid_phase_c(K, wbeg[me], nw_me, hrecv.as<uint64_t>(), hout.data(), hF.data(),
+                               &rs, stream);
+        for (int64_t i = 0; i < nlocal; ++i) F[i] = hout[local_to_global[i]] + hF[i];
       } else if (nlocal) {
         rs = RunStats();
         solver->run(nlocal, local.off.data(), local.ids.data(), F.data(), a.json ? E2.data() : nullptr,

@@ -48,6 +48,32 @@ T* dup(const std::vector<T>& v) {
 hipStream_t as_stream(void* s) { return (hipStream_t)s; }
 }  // namespace
 
+// run fn on the solver's device stream with event timing and fill st
+template <class Fn>
+void timed(msbfs_solver s, void* stream, msbfs_stats* st, Fn&& fn) {
+  MSBFS_HIP_CHECK(hipSetDevice(s->graph->g.device));
+  msbfs::RunStats rs;
+  hipStream_t hs = as_stream(stream);
+  hipEvent_t e0, e1;
+  MSBFS_HIP_CHECK(hipEventCreate(&e0));
+  MSBFS_HIP_CHECK(hipEventCreate(&e1));
+  MSBFS_HIP_CHECK(hipEventRecord(e0, hs));
+  fn(&rs, hs);
+  MSBFS_HIP_CHECK(hipEventRecord(e1, hs));
+  MSBFS_HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  MSBFS_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (st) {
+    st->levels = rs.levels;
+    st->td_levels = rs.td_levels;
+    st->bu_levels = rs.bu_levels;
+    st->batches = rs.batches;
+    st->device_ms = ms;
+  }
+}
+
 extern "C" {
 
 const char* msbfs_last_error(void) { return g_err.c_str(); }
@@ -350,27 +376,40 @@ int msbfs_solver_set_options(msbfs_solver s, const msbfs_options* o) {
 int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32_t* qids,
                      int64_t* F, int64_t* edges2, msbfs_stats* st, void* stream) {
   return guard([&] {
-    MSBFS_HIP_CHECK(hipSetDevice(s->graph->g.device));
-    msbfs::RunStats rs;
-    hipStream_t hs = as_stream(stream);
-    hipEvent_t e0, e1;
-    MSBFS_HIP_CHECK(hipEventCreate(&e0));
-    MSBFS_HIP_CHECK(hipEventCreate(&e1));
-    MSBFS_HIP_CHECK(hipEventRecord(e0, hs));
-    s->impl->run(K, qoff, qids, F, edges2, &rs, hs);
-    MSBFS_HIP_CHECK(hipEventRecord(e1, hs));
-    MSBFS_HIP_CHECK(hipEventSynchronize(e1));
-    float ms = 0;
-    MSBFS_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    if (st) {
-      st->levels = rs.levels;
-      st->td_levels = rs.td_levels;
-      st->bu_levels = rs.bu_levels;
-      st->batches = rs.batches;
-      st->device_ms = ms;
-    }
+    timed(s, stream, st, [&](msbfs::RunStats* rs, hipStream_t hs) {
+      s->impl->run(K, qoff, qids, F, edges2, rs, hs);
+    });
+  });
+}
+
+int msbfs_hybrid_split(msbfs_graph g, int nparts, int64_t vertex_weight, int64_t* bounds) {
+  return guard([&] { msbfs::hybrid_split(g->g, nparts, vertex_weight, bounds); });
+}
+
+int64_t msbfs_solver_hybrid_max_groups(msbfs_solver s) {
+  return s && s->impl ? s->impl->hybrid_max_groups() : 0;
+}
+
+int msbfs_solver_hybrid_phase_a(msbfs_solver s, int64_t K, const int64_t* qoff,
+                                const int32_t* qids, int64_t lo, int64_t hi, int count_l1,
+                                int nparts, const int32_t* wbeg, void* send_dev, int64_t* out,
+                                msbfs_stats* st, void* stream) {
+  return guard([&] {
+    timed(s, stream, st, [&](msbfs::RunStats* rs, hipStream_t hs) {
+      s->impl->hybrid_phase_a(K, qoff, qids, lo, hi, count_l1 != 0, nparts, wbeg,
+                              (uint64_t*)send_dev, out, rs, hs);
+    });
+  });
+}
+
+int msbfs_solver_hybrid_phase_c(msbfs_solver s, int64_t K, int w_begin, int w_count,
+                                const void* recv_dev, const int64_t* reduced, int64_t* F_local,
+                                msbfs_stats* st, void* stream) {
+  return guard([&] {
+    timed(s, stream, st, [&](msbfs::RunStats* rs, hipStream_t hs) {
+      s->impl->hybrid_phase_c(K, w_begin, w_count, (const uint64_t*)recv_dev, reduced, F_local,
+                              rs, hs);
+    });
   });
 }
 

@@ -210,7 +210,8 @@ struct BitCounter {
   }
 };
 
-// Sum the level's slab rows: block (word, row-group); lane = group bit. F += level * count,
+// Sum the level's slab rows: block (word, row-group); lane = group bit. F += level * count
+// (`level` is the weight: 0 for a level another rank of the hybrid mode accounts for),
 // alive_next |= groups with count > 0 (one ballot + one atomicOr per word per row-group).
 template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
@@ -443,8 +444,10 @@ __global__ __launch_bounds__(kBlock) void k_zero_acc(const int32_t* fl, int64_t 
   }
 }
 
-// build the bottom-up active lists (deg > 0, not done), split by degree
-__global__ __launch_bounds__(kBlock) void k_build_active(int64_t n, const int64_t* rowptr,
+// build the bottom-up active lists (deg > 0, not done) over the vertex range [lo, hi), split
+// by degree (the hybrid mode's vertex-partitioned level pulls only for its own range)
+__global__ __launch_bounds__(kBlock) void k_build_active(int64_t lo, int64_t hi,
+                                                         const int64_t* rowptr,
                                                          const uint32_t* done, int wide_deg,
                                                          int32_t* act, int32_t* actw, Ctr* ctr) {
   __shared__ LdsQueue qn, qw;
@@ -453,11 +456,11 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t n, const int64_
   q_init(qw);
   __syncthreads();
   unsigned long long eu = 0;
-  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < n; b += (int64_t)gridDim.x * kBlock) {
+  for (int64_t b = lo + (int64_t)blockIdx.x * kBlock; b < hi; b += (int64_t)gridDim.x * kBlock) {
     const int64_t i = b + threadIdx.x;
     int64_t d = 0;
     bool ok = false;
-    if (i < n) {
+    if (i < hi) {
       d = rowptr[i + 1] - rowptr[i];
       ok = d > 0 && !is_done(done, (int32_t)i);
     }
@@ -850,6 +853,92 @@ __global__ __launch_bounds__(kBlock) void k_count_frontier(const int32_t* fl, co
 }
 
 // ---------------------------------------------------------------------------------------------
+// hybrid multi-GPU mode: kernels
+//
+// Why: with groups split round-robin over GPUs (main.cu:304-307) every GPU still scans the whole
+// graph at the first bottom-up level, whose cost hardly depends on the number of groups (a row
+// scan stops only once EVERY group is covered), so 8 GPUs each pay most of one GPU's time. Levels
+// 1-2 need only the sources' neighbourhoods, which every rank can build for all groups, so level
+// 2 is split by vertex range (each rank pulls 1/N of the edges for all groups) and one
+// all-to-all then gives every rank its own block of words for every vertex (hybrid 2D
+// decomposition: vertex-partitioned for the explosive level, query-partitioned after it).
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxParts = 64;
+struct WordSplit {
+  int32_t b[kMaxParts + 1];
+};
+
+// send[(hi-lo)*wbeg[j] + (v-lo)*nw_j + (w-wbeg[j])] = vis[v*W + w]: destination-major blocks
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, int64_t lo,
+                                                       int64_t cnt, int wt, WordSplit ws,
+                                                       uint64_t* send) {
+  const int64_t total = cnt * wt;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t i = t / wt;
+    const int w = (int)(t - i * wt);
+    int j = 0;
+    while (w >= ws.b[j + 1]) ++j;
+    const int nw = ws.b[j + 1] - ws.b[j];
+    send[cnt * ws.b[j] + i * nw + (w - ws.b[j])] = vis[(lo + i) * W + w];
+  }
+}
+
+// Phase C state from the received words: both visited buffers (stride W, zero padding beyond
+// nw), done = every alive group present, anyvis = any bit. One thread per vertex; the bitmaps
+// are written with plain stores from wave ballots (64 vertices = 2 words), so no memset.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, int nw, int64_t n,
+                                                         uint64_t* visA, uint64_t* visB,
+                                                         const uint64_t* alive,
+                                                         const uint64_t* gmask, uint32_t* done,
+                                                         uint32_t* anyvis) {
+  const int64_t nwords32 = (n + 31) / 32;
+  uint64_t am[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) am[w] = alive[w] & gmask[w];
+  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < n; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t v = b + threadIdx.x;
+    bool full = false, nz = false;
+    if (v < n) {
+      full = true;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const uint64_t x = w < nw ? recv[v * nw + w] : 0ull;
+        visA[v * W + w] = x;
+        visB[v * W + w] = x;
+        nz |= x != 0;
+        full &= (~x & am[w]) == 0;
+      }
+    }
+    const uint64_t bd = __ballot(full), ba = __ballot(nz);
+    const int lane = lane_id();
+    const int64_t w32 = (b + (threadIdx.x & ~63)) >> 5;
+    if (lane < 2 && w32 + lane < nwords32) {
+      done[w32 + lane] = (uint32_t)(bd >> (32 * lane));
+      anyvis[w32 + lane] = (uint32_t)(ba >> (32 * lane));
+    }
+  }
+}
+
+// bounds[p] = first v with rowptr[v] + vw*v >= p/nparts of the total (bounds[0]=0, [nparts]=n)
+__global__ void k_split_bounds(const int64_t* rowptr, int64_t n, int nparts, int64_t vw,
+                               int64_t* bounds) {
+  const int p = (int)threadIdx.x;
+  if (p > nparts) return;
+  const int64_t total = rowptr[n] + vw * n;
+  const int64_t target = total / nparts * p + total % nparts * p / nparts;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rowptr[mid] + vw * mid >= target) hi = mid;
+    else lo = mid + 1;
+  }
+  bounds[p] = p == 0 ? 0 : (p == nparts ? n : lo);
+}
+
+// ---------------------------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------------------------
 class BitparSolver final : public Solver {
@@ -897,6 +986,7 @@ class BitparSolver final : public Solver {
     slabF_.alloc((size_t)3 * kMaxGrid * 64 * maxW_ * sizeof(uint32_t));
     slabE_.alloc((size_t)3 * kMaxGrid * 64 * maxW_ * sizeof(unsigned long long));
     hctr_ = std::make_unique<PinnedBuf>(sizeof(Ctr));
+    hsmall_ = std::make_unique<PinnedBuf>(small_.bytes);
     if (const char* d = getenv("MSBFS_DIRS")) dirs_ = d;  // per-level T/B override (tuning)
     if (const char* u = getenv("MSBFS_UNROLL")) unroll_ = atoi(u);
     if (const char* w = getenv("MSBFS_WIDE_LATER")) wide_later_ = atoi(w);
@@ -917,10 +1007,111 @@ class BitparSolver final : public Solver {
     }
   }
 
+  int64_t hybrid_max_groups() const override { return 64 * (int64_t)maxW_; }
+
+  void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t lo, int64_t hi,
+                      bool count_l1, int nparts, const int32_t* wbeg, uint64_t* send,
+                      int64_t* out, RunStats* st, hipStream_t s) override {
+    if (K < 1 || K > hybrid_max_groups())
+      fail("hybrid mode: K=" + std::to_string(K) + " groups exceeds one round (" +
+           std::to_string(hybrid_max_groups()) + ")");
+    if (lo < 0 || hi < lo || hi > g_.n) fail("hybrid mode: bad vertex range");
+    if (nparts < 1 || nparts > kMaxParts) fail("hybrid mode: 1..64 ranks");
+    const int wt = (int)((K + 63) / 64);
+    if (wbeg[0] != 0 || wbeg[nparts] != wt) fail("hybrid mode: word split must cover ceil(K/64)");
+    for (int j = 0; j < nparts; ++j)
+      if (wbeg[j + 1] < wbeg[j]) fail("hybrid mode: word split not monotone");
+    int w = 1;
+    while (w < wt) w <<= 1;
+#define MSBFS_BP_CASE(WW)                                                                  \
+  case WW:                                                                                 \
+    phase_a_impl<WW>(K, qoff, qids, lo, hi, count_l1, nparts, wbeg, send, out, st, s);     \
+    break;
+    switch (w) {
+      MSBFS_BP_CASE(1)
+      MSBFS_BP_CASE(2)
+      MSBFS_BP_CASE(4)
+      MSBFS_BP_CASE(8)
+      MSBFS_BP_CASE(16)
+      default: fail("bad word count");
+    }
+#undef MSBFS_BP_CASE
+    if (st) st->batches++;
+  }
+
+  void hybrid_phase_c(int64_t K, int w_begin, int w_count, const uint64_t* recv,
+                      const int64_t* reduced, int64_t* F_out, RunStats* st,
+                      hipStream_t s) override {
+    if (w_count <= 0) return;
+    if (w_begin < 0 || (int64_t)(w_begin + w_count) * 64 - 63 > K || w_count > maxW_)
+      fail("hybrid mode: bad word block");
+    int w = 1;
+    while (w < w_count) w <<= 1;
+#define MSBFS_BP_CASE(WW)                                                          \
+  case WW:                                                                         \
+    phase_c_impl<WW>(K, w_begin, w_count, recv, reduced, F_out, st, s);            \
+    break;
+    switch (w) {
+      MSBFS_BP_CASE(1)
+      MSBFS_BP_CASE(2)
+      MSBFS_BP_CASE(4)
+      MSBFS_BP_CASE(8)
+      MSBFS_BP_CASE(16)
+      default: fail("bad word count");
+    }
+#undef MSBFS_BP_CASE
+  }
+
  private:
+  // Level-loop state. The normal path runs one batch start to finish; the hybrid phases run
+  // a capped / range-restricted piece of it (phase A) or resume it from exchanged state (C).
+  struct Loop {
+    int cur = 0;  // vis_[cur] = read buffer (up to date for every non-done vertex)
+    int fc = 0;   // fl_[fc] = current frontier
+    int ac = 0;   // acc_[ac] holds the current frontier bits when fsrc_acc
+    int alv = 0;  // alive[alv] = groups with a non-empty frontier
+    uint32_t level = 0;
+    int64_t nf = 0, ef = 0, ev = 0, na = 0, ea = 0, nact = 0, nactw = 0;
+    bool have_active = false, fsrc_acc = true, bottom_up = false;
+    int bu_levels = 0;
+    // limits
+    uint32_t stop_level = 0xFFFFFFFFu;  // last level to run
+    int64_t lo = 0, hi = 0;             // vertex range of the first active-list build
+    bool weight_l1 = true;              // add level-1 counts to F
+    std::string plan;                   // plan[level] = 'T'/'B' forces the next level
+    int64_t ev_l1 = 0;                  // ev after level 1
+  };
+  struct Small {
+    unsigned long long* F;
+    unsigned long long* E;
+    uint64_t* alive[2];
+    uint64_t* gmask;
+  };
+  Small small() {
+    Small r;
+    r.F = small_.as<unsigned long long>();
+    r.E = r.F + 64 * 16;
+    r.alive[0] = (uint64_t*)(r.E + 64 * 16);
+    r.alive[1] = r.alive[0] + 16;
+    r.gmask = r.alive[1] + 16;
+    return r;
+  }
+
+  template <int W, bool COUNT>
+  void start_batch(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids, Loop& S,
+                   hipStream_t s);
+  template <int W, bool COUNT>
+  void levels(Loop& S, RunStats* st, hipStream_t s);
   template <int W, bool COUNT>
   void batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids, int64_t* F,
                   int64_t* edges2, RunStats* st, hipStream_t s);
+  template <int W>
+  void phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t lo, int64_t hi,
+                    bool count_l1, int nparts, const int32_t* wbeg, uint64_t* send, int64_t* out,
+                    RunStats* st, hipStream_t s);
+  template <int W>
+  void phase_c_impl(int64_t K, int w_begin, int w_count, const uint64_t* recv,
+                    const int64_t* reduced, int64_t* F_out, RunStats* st, hipStream_t s);
 
   void run_batch(int w, int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
                  int64_t* F, int64_t* edges2, RunStats* st, hipStream_t s) {
@@ -948,41 +1139,45 @@ class BitparSolver final : public Solver {
     return HostCtr{c->act2.v, c->actw2.v, c->fl2.v, c->touched.v, c->ef2.v, c->eu2.v, c->ev2.v};
   }
 
+  // copy the small block (F, E, alive, gmask) to pinned host memory and wait
+  const unsigned long long* read_small(hipStream_t s) {
+    MSBFS_HIP_CHECK(hipMemcpyAsync(hsmall_->p, small_.p, small_.bytes, hipMemcpyDeviceToHost, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    return hsmall_->as<unsigned long long>();
+  }
+
   const DeviceGraph& g_;
   int maxW_ = 1;
   DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
       ctr_, small_, pairs_, slabF_, slabE_, anyvis_;
-  double filter_frac_ = 0.5;
-  double hub_bytes_ = 0.0;  // MSBFS_HUB_MB: hub rows loaded without the bitmap test (measured: off is best)  // skip unvisited neighbours while visited edges < frac * nnz
+  double filter_frac_ = 0.5;  // skip unvisited neighbours while visited edges < frac * nnz
+  double hub_bytes_ = 0.0;    // MSBFS_HUB_MB: hub rows loaded without the bitmap test (off: best)
   size_t scan_bytes_ = 0;
-  std::unique_ptr<PinnedBuf> hctr_;
+  std::unique_ptr<PinnedBuf> hctr_, hsmall_;
   int32_t epoch_ = 0;
   std::string dirs_;
   int unroll_ = 8;
   int wide_later_ = 1024;
 };
 
+// per-batch reset + sources + level 0 (k_init); leaves the loop state ready for level 1
 template <int W, bool COUNT>
-void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
-                              int64_t* Fout, int64_t* edges2, RunStats* st, hipStream_t s) {
-  using L = Lay<W>;
+void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
+                               Loop& S, hipStream_t s) {
   const int64_t n = g_.n;
   const size_t vb = (size_t)std::max<int64_t>(n, 1) * W * sizeof(uint64_t);
-  // ---- per-batch state reset
   MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(vis_[1].p, 0, vb, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(done_.p, 0, done_.bytes, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(anyvis_.p, 0, anyvis_.bytes, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
   MSBFS_HIP_CHECK(hipMemsetAsync(small_.p, 0, small_.bytes, s));
-  unsigned long long* dF = small_.as<unsigned long long>();
-  unsigned long long* dE = dF + 64 * 16;
-  uint64_t* alive[2] = {(uint64_t*)(dE + 64 * 16), (uint64_t*)(dE + 64 * 16) + 16};
-  uint64_t* gmask = alive[1] + 16;
+  const Small sm = small();
   {
     uint64_t hm[16] = {0};
     for (int64_t k = 0; k < nb; ++k) hm[k >> 6] |= 1ull << (k & 63);
-    MSBFS_HIP_CHECK(hipMemcpyAsync(gmask, hm, sizeof(hm), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, hm, sizeof(hm), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));  // hm is a stack buffer
   }
   // ---- sources: (vertex, local group) pairs, out-of-range ids dropped (main.cu:49)
   std::vector<int32_t> hp, hk;
@@ -1005,199 +1200,314 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
     MSBFS_HIP_CHECK(hipMemcpyAsync(dpk, hp.data() + np, np * sizeof(int32_t),
                                    hipMemcpyHostToDevice, s));
   }
-  int cur = 0;  // vis_[cur] = read buffer (up to date for every non-done vertex)
-  int fc = 0;   // fl_[fc] = current frontier
-  int ac = 0;   // acc_[ac] holds the current frontier bits when fsrc_acc
   ++epoch_;
   if (np) {
     k_init<W, COUNT><<<grid_for(np, kBlock), kBlock, 0, s>>>(
         dpv, dpk, np, g_.rowptr, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
-        acc_[ac].as<uint64_t>(), stamp_.as<int32_t>(), epoch_, fl_[fc].as<int32_t>(),
-        ctr_.as<Ctr>(), dE, alive[0], anyvis_.as<uint32_t>(), g_.old2new);
+        acc_[S.ac].as<uint64_t>(), stamp_.as<int32_t>(), epoch_, fl_[S.fc].as<int32_t>(),
+        ctr_.as<Ctr>(), sm.E, sm.alive[0], anyvis_.as<uint32_t>(), g_.old2new);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
-  HostCtr c = read_ctr(s);
-  int64_t nf = c.fl2, ef = (int64_t)c.ef2;
-  int64_t ev = (int64_t)c.ev2;  // degree sum of vertices visited by any group so far
-  int64_t na = n, ea = g_.nnz;  // active estimate before the first bottom-up build
-  int64_t nact = 0, nactw = 0;
-  bool have_active = false, fsrc_acc = true, bottom_up = false;
-  int st_bu_levels = 0;
-  int alv = 0;
-  uint32_t level = 0;
+  const HostCtr c = read_ctr(s);  // also retires the pinned/host source copies
+  S.nf = c.fl2;
+  S.ef = (int64_t)c.ef2;
+  S.ev = (int64_t)c.ev2;
+  S.na = n;
+  S.ea = g_.nnz;  // active estimate before the first bottom-up build
+}
+
+template <int W, bool COUNT>
+void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
+  using L = Lay<W>;
+  const int64_t n = g_.n;
+  const Small sm = small();
   const int grid = kMaxGrid;
   static const bool trace = getenv("MSBFS_TRACE") != nullptr;
   auto tl = std::chrono::steady_clock::now();
-  while (nf > 0) {
+  HostCtr c{};
+  while (S.nf > 0 && S.level < S.stop_level) {
     // direction choice (Beamer et al. SC'12, on the union frontier)
+    bool& bottom_up = S.bottom_up;
     if (opt.force_dir == 1) bottom_up = false;
-    else if (opt.force_dir == 2) bottom_up = level > 0;
-    else if (!bottom_up) bottom_up = (double)ef > (double)ea / opt.alpha;
-    else bottom_up = !((double)nf < (double)na / opt.beta && (double)ef < (double)ea / opt.alpha);
-    if (level < dirs_.size() && (dirs_[level] == 'T' || dirs_[level] == 'B'))
-      bottom_up = dirs_[level] == 'B';
+    else if (opt.force_dir == 2) bottom_up = S.level > 0;
+    else if (!bottom_up) bottom_up = (double)S.ef > (double)S.ea / opt.alpha;
+    else bottom_up = !((double)S.nf < (double)S.na / opt.beta && (double)S.ef < (double)S.ea / opt.alpha);
+    if (S.level < dirs_.size() && (dirs_[S.level] == 'T' || dirs_[S.level] == 'B'))
+      bottom_up = dirs_[S.level] == 'B';
+    if (S.level < S.plan.size() && (S.plan[S.level] == 'T' || S.plan[S.level] == 'B'))
+      bottom_up = S.plan[S.level] == 'B';
     MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
-    MSBFS_HIP_CHECK(hipMemsetAsync(alive[alv ^ 1], 0, 16 * sizeof(uint64_t), s));
-    ++level;
+    MSBFS_HIP_CHECK(hipMemsetAsync(sm.alive[S.alv ^ 1], 0, 16 * sizeof(uint64_t), s));
+    ++S.level;
     int rows = 0;  // slab rows written by this level's counting kernels
     auto slabF = [&](int r) { return slabF_.as<uint32_t>() + (size_t)r * 64 * W; };
     auto slabE = [&](int r) { return slabE_.as<unsigned long long>() + (size_t)r * 64 * W; };
-    uint64_t* R = vis_[cur].as<uint64_t>();
-    uint64_t* O = vis_[cur ^ 1].as<uint64_t>();
+    uint64_t* R = vis_[S.cur].as<uint64_t>();
+    uint64_t* O = vis_[S.cur ^ 1].as<uint64_t>();
+    const uint64_t* alive = sm.alive[S.alv];
     if (!bottom_up) {
       // ---- top-down
-      frontier_degree_scan(g_.rowptr, fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(),
+      frontier_degree_scan(g_.rowptr, fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(),
                            scan_tmp_.p, scan_bytes_, s);
       ++epoch_;
-      const int eg = grid_for(ef, L::TILE, 8192);
-      if (fsrc_acc)
+      const int eg = grid_for(S.ef, L::TILE, 8192);
+      if (S.fsrc_acc)
         k_td_expand<W, false><<<eg, kBlock, 0, s>>>(
-            fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
-            acc_[ac].as<uint64_t>(), done_.as<uint32_t>(), acc_[ac ^ 1].as<uint64_t>(),
+            fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
+            acc_[S.ac].as<uint64_t>(), done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(),
             stamp_.as<int32_t>(), epoch_, touched_.as<int32_t>(), ctr_.as<Ctr>());
       else
         k_td_expand<W, true><<<eg, kBlock, 0, s>>>(
-            fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R, O,
-            done_.as<uint32_t>(), acc_[ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
+            fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R, O,
+            done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
             touched_.as<int32_t>(), ctr_.as<Ctr>());
       MSBFS_HIP_CHECK(hipGetLastError());
       // touched <= min(n, frontier edges); the kernel reads the exact count from ctr
-      const int64_t nt_max = std::min<int64_t>(std::max<int64_t>(ef, nf), n);
+      const int64_t nt_max = std::min<int64_t>(std::max<int64_t>(S.ef, S.nf), n);
       const int gf = grid_for(nt_max, L::TILE, grid);
       k_td_finalize<W, COUNT><<<gf, kBlock, 0, s>>>(
-          touched_.as<int32_t>(), g_.rowptr, R, O, acc_[ac ^ 1].as<uint64_t>(), alive[alv],
-          gmask, done_.as<uint32_t>(), fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
-          fl_[fc].as<int32_t>(), nf, fsrc_acc ? acc_[ac].as<uint64_t>() : nullptr,
+          touched_.as<int32_t>(), g_.rowptr, R, O, acc_[S.ac ^ 1].as<uint64_t>(), alive,
+          sm.gmask, done_.as<uint32_t>(), fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+          fl_[S.fc].as<int32_t>(), S.nf, S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr,
           anyvis_.as<uint32_t>());
       MSBFS_HIP_CHECK(hipGetLastError());
       // new frontier bits are in acc_[ac ^ 1]
       const int gc = grid_for(nt_max, L::TILE, grid);
       k_count_frontier<W, COUNT, false><<<gc, kBlock, 0, s>>>(
-          fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), g_.rowptr, acc_[ac ^ 1].as<uint64_t>(),
+          fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), g_.rowptr, acc_[S.ac ^ 1].as<uint64_t>(),
           nullptr, slabF(rows), slabE(rows));
       rows += gc;
       MSBFS_HIP_CHECK(hipGetLastError());
-      ac ^= 1;
-      fsrc_acc = true;
+      S.ac ^= 1;
+      S.fsrc_acc = true;
       if (st) st->td_levels++;
     } else {
       // ---- bottom-up
-      if (!have_active) {
-        k_build_active<<<grid_for(n, kBlock), kBlock, 0, s>>>(
-            n, g_.rowptr, done_.as<uint32_t>(), opt.wide_degree, act_[0].as<int32_t>(),
+      const int next_wide = std::max(opt.wide_degree, wide_later_);
+      if (!S.have_active) {
+        // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
+        // off only for much higher degrees, so later lists are split at a higher threshold
+        const int wide0 = S.bu_levels == 0 ? opt.wide_degree : next_wide;
+        k_build_active<<<grid_for(S.hi - S.lo, kBlock), kBlock, 0, s>>>(
+            S.lo, S.hi, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
             actw_[0].as<int32_t>(), ctr_.as<Ctr>());
         MSBFS_HIP_CHECK(hipGetLastError());
         c = read_ctr(s);
-        nact = c.act2;
-        nactw = c.actw2;
-        have_active = true;
+        S.nact = c.act2;
+        S.nactw = c.actw2;
+        S.have_active = true;
         MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
       }
-      const bool first_bu = st_bu_levels == 0;
-      ++st_bu_levels;
-      if (fsrc_acc) {
+      const bool first_bu = S.bu_levels == 0;
+      ++S.bu_levels;
+      if (S.fsrc_acc) {
         // bottom-up does not read frontier bits; clear the pending top-down ones so acc_[ac]
         // is all-zero and can collect the wide vertices' chunk results
-        k_zero_acc<W><<<grid_for(nf * L::G, kBlock), kBlock, 0, s>>>(
-            fl_[fc].as<int32_t>(), nf, acc_[ac].as<uint64_t>());
+        k_zero_acc<W><<<grid_for(S.nf * L::G, kBlock), kBlock, 0, s>>>(
+            fl_[S.fc].as<int32_t>(), S.nf, acc_[S.ac].as<uint64_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
       }
-      const bool filter = (double)ev < filter_frac_ * (double)g_.nnz;
+      const bool filter = (double)S.ev < filter_frac_ * (double)g_.nnz;
       // hub rows (lowest ids after degree relabelling) sized to ~hub_bytes_ are always loaded
       const int64_t hub_ids = g_.old2new ? (int64_t)(hub_bytes_ / (8.0 * W)) : 0;
       const int32_t filter_from =
           filter ? (int32_t)std::min<int64_t>(hub_ids, INT32_MAX) : INT32_MAX;
-      // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
-      // off only for much higher degrees, so the next lists are split at a higher threshold
-      const int next_wide = std::max(opt.wide_degree, wide_later_);
-      if (nact) {
+      if (S.nact) {
         auto kern = unroll_ >= 8 ? k_bu_narrow<W, COUNT, 8> : k_bu_narrow<W, COUNT, 4>;
-        const int gn = grid_for(nact, L::TILE, grid);
-        kern<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), nact, g_.rowptr, g_.col, R, O, alive[alv],
-                                   gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
-                                   fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+        const int gn = grid_for(S.nact, L::TILE, grid);
+        kern<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
+                                   sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
+                                   fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                    anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
                                    next_wide);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
-      if (nactw) {
-        frontier_degree_scan(g_.rowptr, actw_[0].as<int32_t>(), nactw, offs_.as<int64_t>(),
+      if (S.nactw) {
+        frontier_degree_scan(g_.rowptr, actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(),
                              scan_tmp_.p, scan_bytes_, s, kChunk);
-        const int64_t chunks_max = nactw + ea / kChunk + 1;
+        const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
         k_bu_chunks<W><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
-            actw_[0].as<int32_t>(), nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
-            alive[alv], gmask, acc_[ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
+            actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
+            sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
             first_bu ? 0 : 1);
         MSBFS_HIP_CHECK(hipGetLastError());
-        const int gw = grid_for(nactw, L::TILE, grid);
+        const int gw = grid_for(S.nactw, L::TILE, grid);
         k_bu_wide_finalize<W, COUNT><<<gw, kBlock, 0, s>>>(
-            actw_[0].as<int32_t>(), nactw, g_.rowptr, R, O, acc_[ac].as<uint64_t>(), alive[alv],
-            gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(),
+            actw_[0].as<int32_t>(), S.nactw, g_.rowptr, R, O, acc_[S.ac].as<uint64_t>(), alive,
+            sm.gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
             ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), act_[1].as<int32_t>(), next_wide);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       {
         // new frontier bits = Wb & ~R (both still in place: the swap is below)
-        const int gc = grid_for(nact + nactw, L::TILE, grid);
+        const int gc = grid_for(S.nact + S.nactw, L::TILE, grid);
         k_count_frontier<W, COUNT, true><<<gc, kBlock, 0, s>>>(
-            fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), g_.rowptr, O, R, slabF(rows), slabE(rows));
+            fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), g_.rowptr, O, R, slabF(rows),
+            slabE(rows));
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gc;
       }
       std::swap(act_[0], act_[1]);
       std::swap(actw_[0], actw_[1]);
-      cur ^= 1;
-      fsrc_acc = false;
+      S.cur ^= 1;
+      S.fsrc_acc = false;
       if (st) st->bu_levels++;
     }
     if (rows) {
       const int rg = std::max(1, std::min(64, rows / 32));
-      k_level_reduce<W, COUNT><<<W * rg, kBlock, 0, s>>>(slabF(0), slabE(0), rows, rg, dF, dE,
-                                                         alive[alv ^ 1], level);
+      const uint32_t weight = (S.level == 1 && !S.weight_l1) ? 0u : S.level;
+      k_level_reduce<W, COUNT><<<W * rg, kBlock, 0, s>>>(slabF(0), slabE(0), rows, rg, sm.F, sm.E,
+                                                         sm.alive[S.alv ^ 1], weight);
       MSBFS_HIP_CHECK(hipGetLastError());
     }
     c = read_ctr(s);
     if (bottom_up) {
-      nact = c.act2;
-      nactw = c.actw2;
-      na = nact + nactw;
-      ea = (int64_t)c.eu2;
+      S.nact = c.act2;
+      S.nactw = c.actw2;
+      S.na = S.nact + S.nactw;
+      S.ea = (int64_t)c.eu2;
     }
     if (trace) {
       const auto t2 = std::chrono::steady_clock::now();
       fprintf(stderr,
               "[msbfs bp W=%d] level %u %s nf=%lld ef=%lld -> nf'=%lld ef'=%lld touched=%u "
               "active=%lld (wide %lld) ea=%lld ev=%lld  %.3f ms\n",
-              W, level, bottom_up ? "BU" : "TD", (long long)nf, (long long)ef,
-              (long long)c.fl2, (long long)c.ef2, c.touched, (long long)na, (long long)nactw,
-              (long long)ea, (long long)(ev + (long long)c.ev2), std::chrono::duration<double, std::milli>(t2 - tl).count());
+              W, S.level, bottom_up ? "BU" : "TD", (long long)S.nf, (long long)S.ef,
+              (long long)c.fl2, (long long)c.ef2, c.touched, (long long)S.na, (long long)S.nactw,
+              (long long)S.ea, (long long)(S.ev + (long long)c.ev2),
+              std::chrono::duration<double, std::milli>(t2 - tl).count());
       tl = t2;
     }
-    nf = c.fl2;
-    ef = (int64_t)c.ef2;
-    ev += (int64_t)c.ev2;
-    fc ^= 1;
-    alv ^= 1;
+    S.nf = c.fl2;
+    S.ef = (int64_t)c.ef2;
+    S.ev += (int64_t)c.ev2;
+    if (S.level == 1) S.ev_l1 = S.ev;
+    S.fc ^= 1;
+    S.alv ^= 1;
     if (st) st->levels++;
   }
+}
+
+template <int W, bool COUNT>
+void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
+                              int64_t* Fout, int64_t* edges2, RunStats* st, hipStream_t s) {
+  Loop S;
+  S.lo = 0;
+  S.hi = g_.n;
+  start_batch<W, COUNT>(k0, nb, qoff, qids, S, s);
+  levels<W, COUNT>(S, st, s);
   // frontier is empty: accumulator entries were cleared by finalize / zero_acc
-  std::vector<unsigned long long> hF(64 * 16), hE(64 * 16);
-  MSBFS_HIP_CHECK(hipMemcpyAsync(hF.data(), dF, 64 * 16 * sizeof(unsigned long long),
-                                 hipMemcpyDeviceToHost, s));
-  if (edges2)
-    MSBFS_HIP_CHECK(hipMemcpyAsync(hE.data(), dE, 64 * 16 * sizeof(unsigned long long),
-                                   hipMemcpyDeviceToHost, s));
-  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  const unsigned long long* h = read_small(s);
   for (int64_t k = 0; k < nb; ++k) {
-    Fout[k] = (int64_t)hF[k];
-    if (edges2) edges2[k] = (int64_t)hE[k];
+    Fout[k] = (int64_t)h[k];
+    if (edges2) edges2[k] = (int64_t)h[64 * 16 + k];
   }
+}
+
+// Phase A: level 1 (top-down, every rank identical, only rank 0 adds it to F), level 2
+// (bottom-up over this rank's vertex range only), then pack this range's words per destination.
+template <int W>
+void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t lo,
+                                int64_t hi, bool count_l1, int nparts, const int32_t* wbeg,
+                                uint64_t* send, int64_t* out, RunStats* st, hipStream_t s) {
+  Loop S;
+  S.lo = lo;
+  S.hi = hi;
+  S.stop_level = 2;
+  S.weight_l1 = count_l1;
+  S.plan = "TB";
+  start_batch<W, false>(0, K, qoff, qids, S, s);
+  levels<W, false>(S, st, s);
+  if (S.fsrc_acc && S.nf > 0) {  // stopped after a top-down level: restore the zero accumulator
+    k_zero_acc<W><<<grid_for(S.nf * Lay<W>::G, kBlock), kBlock, 0, s>>>(
+        fl_[S.fc].as<int32_t>(), S.nf, acc_[S.ac].as<uint64_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  const int wt = (int)((K + 63) / 64);
+  if (hi > lo) {
+    WordSplit ws{};
+    for (int j = 0; j <= nparts; ++j) ws.b[j] = wbeg[j];
+    for (int j = nparts + 1; j <= kMaxParts; ++j) ws.b[j] = wt + 1;  // never reached
+    k_pack_words<W><<<grid_for((hi - lo) * wt, kBlock, 8192), kBlock, 0, s>>>(
+        vis_[S.cur].as<uint64_t>(), lo, hi - lo, wt, ws, send);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  const bool ran_l2 = S.level >= 2;
+  const Small sm = small();
+  const unsigned long long* h = read_small(s);
+  const unsigned long long* alive_h = h + (sm.alive[S.alv] - (uint64_t*)sm.F);
+  for (int64_t k = 0; k < K; ++k) {
+    out[k] = (int64_t)h[k];
+    out[K + k] = ran_l2 ? (int64_t)((alive_h[k >> 6] >> (k & 63)) & 1ull) : 0;
+  }
+  out[2 * K] = ran_l2 ? S.nf : 0;
+  out[2 * K + 1] = ran_l2 ? S.ef : 0;
+  out[2 * K + 2] = count_l1 ? S.ev : (ran_l2 ? S.ev - S.ev_l1 : 0);
+}
+
+// Phase C: rebuild the level-2 state of this rank's groups from the exchanged words and run
+// the remaining levels (the first one bottom-up: the frontier is only implicit in the words).
+template <int W>
+void BitparSolver::phase_c_impl(int64_t K, int w_begin, int w_count, const uint64_t* recv,
+                                const int64_t* reduced, int64_t* F_out, RunStats* st,
+                                hipStream_t s) {
+  const int64_t n = g_.n;
+  MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
+  MSBFS_HIP_CHECK(hipMemsetAsync(small_.p, 0, small_.bytes, s));
+  const Small sm = small();
+  {
+    uint64_t ha[2][16] = {{0}};  // alive, gmask
+    for (int w = 0; w < w_count; ++w)
+      for (int b = 0; b < 64; ++b) {
+        const int64_t k = (int64_t)(w_begin + w) * 64 + b;
+        if (k >= K) break;
+        ha[1][w] |= 1ull << b;
+        if (reduced[K + k] > 0) ha[0][w] |= 1ull << b;
+      }
+    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[0], ha[0], sizeof(ha[0]), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, ha[1], sizeof(ha[1]), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  if (n > 0) {
+    k_hybrid_setup<W><<<grid_for(n, kBlock, 8192), kBlock, 0, s>>>(
+        recv, w_count, n, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(), sm.alive[0], sm.gmask,
+        done_.as<uint32_t>(), anyvis_.as<uint32_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  Loop S;
+  S.lo = 0;
+  S.hi = n;
+  S.level = 2;
+  S.nf = reduced[2 * K];
+  S.ef = reduced[2 * K + 1];
+  S.ev = reduced[2 * K + 2];
+  S.na = n;
+  S.ea = g_.nnz;
+  S.bu_levels = 1;
+  S.fsrc_acc = false;
+  S.bottom_up = true;
+  S.plan = "..B";
+  levels<W, false>(S, st, s);
+  const unsigned long long* h = read_small(s);
+  for (int64_t i = 0; i < (int64_t)w_count * 64; ++i) F_out[i] = (int64_t)h[i];
 }
 
 }  // namespace bp
 
 std::unique_ptr<Solver> make_bitpar_solver(const DeviceGraph& g, int max_groups) {
   return std::make_unique<bp::BitparSolver>(g, max_groups);
+}
+
+void hybrid_split(const DeviceGraph& g, int nparts, int64_t vertex_weight, int64_t* bounds) {
+  if (nparts < 1 || nparts > 1023) fail("hybrid_split: 1..1023 parts");
+  if (vertex_weight < 0) fail("hybrid_split: negative vertex weight");
+  MSBFS_HIP_CHECK(hipSetDevice(g.device));
+  DevBuf d;
+  d.alloc((size_t)(nparts + 1) * sizeof(int64_t));
+  bp::k_split_bounds<<<1, 1024>>>(g.rowptr, g.n, nparts, vertex_weight, d.as<int64_t>());
+  MSBFS_HIP_CHECK(hipGetLastError());
+  MSBFS_HIP_CHECK(hipMemcpy(bounds, d.p, (size_t)(nparts + 1) * sizeof(int64_t),
+                            hipMemcpyDeviceToHost));
 }
 
 }  // namespace msbfs

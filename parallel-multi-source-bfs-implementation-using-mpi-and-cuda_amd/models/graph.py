@@ -213,6 +213,13 @@ class DeviceGraph:
         native.check(native.lib().msbfs_graph_relabel_map(self.handle, native.ptr(out, C.c_int32)))
         return out
 
+    def hybrid_split(self, nparts: int, vertex_weight: int = 8) -> np.ndarray:
+        """Vertex range bounds[0..nparts] balanced on deg(v) + vertex_weight (hybrid mode)."""
+        b = np.zeros(nparts + 1, dtype=np.int64)
+        native.check(native.lib().msbfs_hybrid_split(self.handle, int(nparts), int(vertex_weight),
+                                                     native.ptr(b, C.c_int64)))
+        return b
+
     def download(self) -> Graph:
         rowptr = np.empty(self.n + 1, dtype=np.int64)
         col = np.empty(self.nnz, dtype=np.int32)

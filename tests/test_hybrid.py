@@ -1,0 +1,140 @@
+"""Hybrid multi-GPU decomposition (parallel/hybrid.py): levels 1-2 vertex-partitioned over ranks,
+one all-to-all of visited words, the rest query-partitioned. Must give the exact F of the
+single-process solver for every rank count, group count and graph shape.
+
+CPU tests pin the exchange layout (numpy twins of the pack kernel and of all_to_all_single, and a
+real gloo all_to_all_single with the same split sizes); GPU tests run all ranks' phases in one
+process (emulate_ranks) and compare with the standard bit-parallel solver."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _H():
+    from msbfs.parallel import hybrid
+    return hybrid
+
+
+@pytest.mark.parametrize("K,world", [(1024, 8), (1024, 3), (100, 4), (64, 8), (700, 5), (1, 1)])
+def test_word_split_and_exchange_layout(K, world):
+    H = _H()
+    wbeg = H.word_split(K, world)
+    wt = (K + 63) // 64
+    assert wbeg[0] == 0 and wbeg[-1] == wt and np.all(np.diff(wbeg) >= 0)
+    owned = np.concatenate([H.own_groups(K, wbeg, r) for r in range(world)])
+    assert np.array_equal(owned, np.arange(K))  # every group exactly once, in order
+    rng = np.random.default_rng(K + world)
+    n = 257
+    W = 1
+    while W < wt:
+        W *= 2
+    vis = rng.integers(0, 2**63, size=(n, W), dtype=np.uint64)
+    bounds = np.sort(np.concatenate([[0, n], rng.integers(0, n, world - 1)])).astype(np.int64)
+    sends = [H.pack_words_np(vis, int(bounds[r]), int(bounds[r + 1]), wbeg) for r in range(world)]
+    for r in range(world):
+        ss, rs = H.split_sizes(bounds, wbeg, r)
+        assert sum(ss) == len(sends[r])
+    recvs = H.all_to_all_np(sends, bounds, wbeg)
+    for j in range(world):
+        nw = int(wbeg[j + 1] - wbeg[j])
+        _, rs = H.split_sizes(bounds, wbeg, j)
+        assert len(recvs[j]) == sum(rs) == n * nw
+        # rank j holds its words of every vertex, vertex-major (the phase-C input layout)
+        assert np.array_equal(recvs[j].reshape(n, nw) if nw else recvs[j],
+                              vis[:, wbeg[j]:wbeg[j + 1]].reshape(n, nw) if nw else recvs[j])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _a2a_worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from msbfs.parallel import distributed as D
+    from msbfs.parallel import hybrid as H
+    ctx = D.init_from_env(backend="gloo", use_gpu=False)
+    K, n = 700, 101
+    wbeg = H.word_split(K, world)
+    bounds = np.array([0, 7, 60, n][:world] + [n], dtype=np.int64) if world > 1 else \
+        np.array([0, n], dtype=np.int64)
+    rng = np.random.default_rng(5)
+    vis = rng.integers(0, 2**62, size=(n, 16), dtype=np.uint64)
+    send = H.pack_words_np(vis, int(bounds[rank]), int(bounds[rank + 1]), wbeg)
+    ss, rs = H.split_sizes(bounds, wbeg, rank)
+    r = torch.empty(sum(rs), dtype=torch.int64)
+    dist.all_to_all_single(r, torch.from_numpy(send.view(np.int64)), rs, ss)
+    np.save(os.path.join(out_dir, f"a2a{rank}.npy"), r.numpy())
+    D.shutdown(ctx)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_all_to_all_matches_emulation(tmp_path, world):
+    H = _H()
+    mp.spawn(_a2a_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    K, n = 700, 101
+    wbeg = H.word_split(K, world)
+    rng = np.random.default_rng(5)
+    vis = rng.integers(0, 2**62, size=(n, 16), dtype=np.uint64)
+    for j in range(world):
+        got = np.load(tmp_path / f"a2a{j}.npy").view(np.uint64)
+        want = vis[:, wbeg[j]:wbeg[j + 1]].reshape(-1)
+        assert np.array_equal(got, want)
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU: emulated ranks in one process vs the standard solver
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("K", [1024, 300, 64, 5])
+def test_hybrid_matches_solver_rmat(msbfs_pkg, world, K):
+    m = msbfs_pkg
+    H = _H()
+    dg = m.DeviceGraph.rmat(14, 16, 3, device=0, relabel=True)
+    qs = m.QuerySet.random(dg.n, K, 16, seed=K + world)
+    with m.Solver(dg, "bitpar", max_groups=K) as s:
+        ref = s.run(qs).F
+        got = H.emulate_ranks(s, qs, world)
+        assert np.array_equal(got, ref), (world, K)
+        # buffers are reused: the standard path still works after hybrid phases
+        assert np.array_equal(s.run(qs).F, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_hybrid_matches_cpu_other_graphs(msbfs_pkg, world):
+    """Small components, isolated vertices, invalid source ids, groups that finish before
+    level 2, high-diameter grids."""
+    m = msbfs_pkg
+    H = _H()
+    graphs = [m.Graph.uniform(5000, 2500, 4), m.Graph.grid(40, 60, 0.9, 5, 2),
+              m.Graph.rmat(11, 4, 7)]
+    for g in graphs:
+        qs = m.QuerySet.random(g.n, 200, 3, seed=world)
+        qs = m.QuerySet.from_groups([list(x) + [-1, g.n + 5] for x in qs.groups()] + [[-3], []])
+        ref = m.cpu_bfs(g, qs)
+        with m.Solver(g.to_device(0), "bitpar", max_groups=qs.K) as s:
+            assert np.array_equal(H.emulate_ranks(s, qs, world), ref.F)
+
+
+@pytest.mark.gpu
+def test_hybrid_runner_single_process(msbfs_pkg):
+    m = msbfs_pkg
+    H = _H()
+    dg = m.DeviceGraph.rmat(13, 16, 2, device=0, relabel=True)
+    qs = m.QuerySet.random(dg.n, 512, 8, seed=1)
+    with m.Solver(dg, "bitpar", max_groups=qs.K) as s:
+        ref = s.run(qs).F
+        res = H.hybrid_bfs(s, qs)
+        assert np.array_equal(res.idx, np.arange(qs.K))
+        assert np.array_equal(res.F, ref)

@@ -62,6 +62,11 @@ for s in "$@"; do
              MSBFS_DIRS=TTTBBBBB MSBFS_TRACE=1 step d128_tttb 600 python bench.py --steps 3 --warmup 1 --groups 128
              MSBFS_TRACE=1 step d128_auto 600 python bench.py --steps 3 --warmup 1 --groups 128
              MSBFS_DIRS=TTBBBBBB MSBFS_TRACE=1 step d1024_ttb 600 python bench.py --steps 3 --warmup 1 ;;
+    hybtest) step hybtest 900 python -m pytest tests/test_hybrid.py -m gpu -x -q ;;
+    hybsim) step hybsim 900 python tools/hybrid_sim.py --scale 26 --ranks 2 4 8 ;;
+    hybsim22) step hybsim22 600 python tools/hybrid_sim.py --scale 22 --ranks 2 8 ;;
+    profhyb) export TMPDIR=/tmp; rm -rf gpurun_out/profhyb; step profhyb 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profhyb -o run -- python tools/hybrid_sim.py --scale 26 --ranks 8 --no-roundrobin ;;
+    hyb2) step hyb2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --scale 22 --steps 2 --warmup 1 --backend gloo --dist hybrid ;;
     road2) step road_td 600 python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 256 --force-dir 1
            step road_a2 600 python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 256 --alpha 2
            step road_1024 600 python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 1024 --force-dir 1

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Per-rank cost of the hybrid decomposition on ONE GPU (no multi-GPU box needed).
+
+Runs every rank's phase A (levels 1-2, own vertex range) and phase C (own groups, levels >= 3)
+sequentially on one GPU (parallel/hybrid.py emulate_ranks), checks F against the single-GPU
+solver, and prints per-rank device times plus the all-to-all volume. The estimated N-GPU step
+is max_r(A_r) + exchange + max_r(C_r); the exchange is priced at --a2a-gbps per GPU (receive
+side), an assumption to be replaced by the driver's measured 8-GPU runs. For comparison it also
+times round-robin (each rank runs ceil(K/N) groups on the whole graph).
+
+    python tools/hybrid_sim.py --scale 26 --groups 1024 --ranks 2 4 8
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=26)
+    ap.add_argument("--edgefactor", type=int, default=16)
+    ap.add_argument("--groups", type=int, default=1024)
+    ap.add_argument("--group-size", type=int, default=16)
+    ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--vertex-weight", type=int, default=8)
+    ap.add_argument("--no-roundrobin", action="store_true")
+    ap.add_argument("--a2a-gbps", type=float, default=300.0,
+                    help="assumed per-GPU all-to-all receive bandwidth (GB/s)")
+    args = ap.parse_args()
+
+    import msbfs
+    from msbfs.parallel import distributed as D
+    from msbfs.parallel import hybrid as H
+
+    g = msbfs.DeviceGraph.rmat(args.scale, args.edgefactor, 1, device=0, relabel=True)
+    qs = msbfs.QuerySet.random(g.n, args.groups, args.group_size, 7)
+    with msbfs.Solver(g, "bitpar", max_groups=qs.K) as s:
+        ref = s.run(qs)
+        t = time.perf_counter()
+        ref = s.run(qs)
+        one = (time.perf_counter() - t) * 1e3
+        print(json.dumps({"ranks": 1, "ms": round(one, 3), "device_ms": ref.stats["device_ms"]}),
+              flush=True)
+        for N in args.ranks:
+            H.emulate_ranks(s, qs, N, args.vertex_weight)  # warm
+            tim = []
+            F = H.emulate_ranks(s, qs, N, args.vertex_weight, timings=tim)
+            ok = bool(np.array_equal(F, ref.F))
+            a = max(x["phase_a_ms"] for x in tim)
+            c = max(x["phase_c_ms"] for x in tim)
+            rb = max(x["recv_bytes"] for x in tim)
+            x_ms = rb / (args.a2a_gbps * 1e9) * 1e3
+            rr = [0.0]
+            for r in ([] if args.no_roundrobin else range(N)):
+                sub = qs.subset(D.round_robin(qs.K, r, N))
+                rr.append(s.run(sub).stats["device_ms"])
+            print(json.dumps({
+                "ranks": N, "correct": ok, "phase_a_ms_max": round(a, 3),
+                "phase_c_ms_max": round(c, 3), "a2a_recv_MB_max": round(rb / 2**20, 1),
+                "a2a_ms_est": round(x_ms, 3), "hybrid_est_ms": round(a + x_ms + c, 3),
+                "roundrobin_ms_max": round(max(rr), 3),
+                "per_rank": [{k: (round(v, 3) if isinstance(v, float) else v)
+                              for k, v in x.items()} for x in tim]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
