@@ -53,7 +53,7 @@ def main() -> int:
     ap.add_argument("--dist", default="auto", choices=["auto", "roundrobin", "hybrid"],
                     help="multi-GPU decomposition: round-robin query groups (main.cu:304-307) or "
                          "hybrid (levels 1-2 vertex-partitioned, then query-partitioned); auto = "
-                         "hybrid when N > 1 and the groups fit one bit-parallel pass")
+                         "run each feasible one once (untimed, max over ranks) and time the faster")
     ap.add_argument("--relabel", type=int, default=1,
                     help="renumber vertices by descending degree after generation (preprocessing)")
     args = ap.parse_args()
@@ -78,42 +78,61 @@ def main() -> int:
     qs = msbfs.QuerySet.random(g.n, args.groups, args.group_size, args.qseed)
     solver = msbfs.Solver(g, args.algo, max_groups=qs.K, alpha=args.alpha, beta=args.beta,
                           wide_degree=args.wide_degree, max_words=args.max_words)
-    mode = args.dist
-    if mode == "auto":
-        mode = ("hybrid" if ctx.world > 1 and args.algo == "bitpar"
-                and qs.K <= solver.hybrid_max_groups() else "roundrobin")
-    if mode == "hybrid":
-        runner = H.HybridRunner(solver, qs.K, ctx)
-        local_idx = runner.idx
-    else:
-        local_idx = D.round_robin(qs.K, ctx.rank, ctx.world)
-    local_q = qs.subset(local_idx)
+    hybrid_ok = ctx.world > 1 and args.algo == "bitpar" and qs.K <= solver.hybrid_max_groups()
+    if args.dist == "hybrid" and not hybrid_ok:
+        print("bench: hybrid mode needs >1 rank, --algo bitpar and K <= one pass", file=sys.stderr)
+        return 2
+    candidates = {"auto": ["roundrobin", "hybrid"] if hybrid_ok else ["roundrobin"],
+                  "roundrobin": ["roundrobin"], "hybrid": ["hybrid"]}[args.dist]
+    plans = {}
+    for m in candidates:
+        if m == "hybrid":
+            runner = H.HybridRunner(solver, qs.K, ctx)
+            plans[m] = (runner, runner.idx)
+        else:
+            rr = D.round_robin(qs.K, ctx.rank, ctx.world)
+            plans[m] = (qs.subset(rr), rr)
     torch.cuda.synchronize(dev)
     setup_s = time.perf_counter() - t_setup
 
-    def step():
-        if mode == "hybrid":
+    def step(m):
+        runner = plans[m][0]
+        if m == "hybrid":
             res = runner.run(qs)
             return res.F, res.stats
-        r = solver.run(local_q)
+        r = solver.run(runner)  # round robin: the rank's query subset
         return r.F, r.stats
 
     # untimed: TEPS numerator (traversed edges per group) — also the first warm-up pass
-    r0 = solver.run(local_q, count_edges=True)
+    rr_idx = D.round_robin(qs.K, ctx.rank, ctx.world)
+    r0 = solver.run(qs.subset(rr_idx), count_edges=True)
     total_edges = int(D.allreduce_sum_i64(np.array([int(r0.edges.sum())], np.int64), ctx)[0])
-    F0, _ = step()
-    if not np.array_equal(F0, r0.F):
-        print(f"rank {ctx.rank}: {mode} F differs from the single-GPU pass", file=sys.stderr)
-        return 3
+    # untimed: every candidate decomposition once (correctness check against the round-robin
+    # pass via the gathered F vector, and its time, max over ranks); the fastest one is timed
+    F_ref = D.gather_F(r0.F, rr_idx, qs.K, ctx)
+    cand_ms = {}
+    for m in candidates:
+        D.barrier(ctx)
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        Fm, _ = step(m)
+        torch.cuda.synchronize(dev)
+        cand_ms[m] = D.allreduce_max(time.perf_counter() - t, ctx) * 1e3
+        Fg = D.gather_F(Fm, plans[m][1], qs.K, ctx)  # identical on every rank
+        if not np.array_equal(Fg, F_ref):
+            print(f"rank {ctx.rank}: {m} F differs from the round-robin pass", file=sys.stderr)
+            return 3
+    mode = min(cand_ms, key=cand_ms.get)
+    local_idx = plans[mode][1]
     if args.verify and ctx.rank == 0:
-        nv = min(args.verify, local_q.K)
+        nv = min(args.verify, len(rr_idx))
         with msbfs.Solver(g, "dist") as ds:
-            rv = ds.run(local_q.subset(range(nv)))
+            rv = ds.run(qs.subset(rr_idx[:nv]))
         if not np.array_equal(rv.F, r0.F[:nv]):
             print(f"VERIFY FAILED: bitpar {r0.F[:nv]} vs dist {rv.F}", file=sys.stderr)
             return 3
     for _ in range(max(0, args.warmup)):
-        F, _ = step()
+        F, _ = step(mode)
         D.packed_argmin(F, local_idx, qs.K, ctx)
 
     D.barrier(ctx)
@@ -121,7 +140,7 @@ def main() -> int:
     t0 = time.perf_counter()
     stats = {}
     for _ in range(args.steps):
-        F, stats = step()
+        F, stats = step(mode)
         min_k, min_f = D.packed_argmin(F, local_idx, qs.K, ctx)
     torch.cuda.synchronize(dev)
     D.barrier(ctx)
@@ -156,6 +175,7 @@ def main() -> int:
                 "levels": stats.get("levels"), "td_levels": stats.get("td_levels"),
                 "bu_levels": stats.get("bu_levels"), "batches": stats.get("batches"),
                 "setup_s": round(setup_s, 3), "relabel": relabelled,
+                "candidates_ms": {k: round(v, 3) for k, v in cand_ms.items()},
             },
         }
         print(json.dumps(out), flush=True)

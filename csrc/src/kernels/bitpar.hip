@@ -251,6 +251,23 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
 // init: scatter the batch's sources (v, local group) into both visited buffers and the
 // top-down accumulator; dedupe vertices into the first frontier list via stamps.
 // ---------------------------------------------------------------------------------------------
+// Only vis_[0] is cleared per batch (hipMemset of n*W words); vis_[1] still holds the previous
+// batch's rows and is made valid row by row: k_init ORs sources into both buffers, so their
+// rows are zeroed first; top-down finalize writes both buffers of every touched vertex; the
+// first bottom-up level writes Wb for every active (deg > 0, not done) vertex. Rows of deg-0
+// vertices are never read (no edges lead to them), so after the first bottom-up level both
+// buffers are valid wherever a kernel looks. Saves one n*W*8-byte fill per batch.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_zero_src_rows(const int32_t* pv, int64_t np,
+                                                         const int32_t* relabel, uint64_t* visB) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < np * W;
+       i += (int64_t)gridDim.x * kBlock) {
+    int32_t v = pv[i / W];
+    if (relabel) v = relabel[v];
+    visB[(int64_t)v * W + (i % W)] = 0;
+  }
+}
+
 template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_t* pk, int64_t np,
                                                  const int64_t* rowptr, uint64_t* visA,
@@ -554,7 +571,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
       anynew |= nw.w[j] != 0;
       notfull |= (unv.w[j] & ~nw.w[j]) != 0;
     }
-    if (g_open) {
+    if (valid) {  // also when nothing is open: Wb may hold the previous batch's rows
       V<VW> nv;
 #pragma unroll
       for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
@@ -600,16 +617,29 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
 //      wave), OR-reduce across groups (xor shuffles) and stop once every alive group is covered.
 // The chunk's new bits are merged into acc[v] with atomicOr (k_bu_wide_finalize folds them in).
 // offs = inclusive prefix of chunk counts over the wide list.
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_bu_chunks(
+//
+// HUBW > 0 (levels that filter): the block first copies the visited bitmap of the HUBW*32
+// lowest ids into LDS. After degree relabelling those are the hubs, which carry most edge
+// endpoints (RMAT-26: the top 2^19 ids take roughly two thirds), so most filter probes become
+// LDS reads instead of divergent global loads. The copy is a snapshot taken at kernel start; a
+// bit another kernel of this level sets later belongs to a vertex first visited at this level,
+// whose row in R is still zero, so skipping it is exact. Big blocks (BT threads, 2 per CU)
+// amortise the copy; the grid is persistent (grid-stride over chunks).
+template <int W, int T, int BT, int HUBW>
+__global__ __launch_bounds__(BT) void k_bu_chunks(
     const int32_t* wl, int64_t nw, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, const uint64_t* alive, const uint64_t* gmask, uint64_t* acc,
-    const uint32_t* anyvis, int32_t filter_from, int coop) {
+    const uint32_t* anyvis, int32_t filter_from, int coop, int xmode, const int32_t* owner) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
-  constexpr int T = 256;  // edges per tile
+  // T = edges per tile
   constexpr int PB = 8;   // rows in flight per lane group in phase B
-  __shared__ int32_t tile[kWaves][T];
+  __shared__ int32_t tile[BT / 64][T];
+  __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
+  if constexpr (HUBW > 0) {
+    for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
+    __syncthreads();
+  }
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
   int32_t* lst = tile[threadIdx.x >> 6];
   const int64_t nchunks = offs[nw - 1];
@@ -618,8 +648,17 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  for (int64_t c = wave; c < nchunks; c += nwaves) {
-    const int64_t i = upper_bound_i64(offs, nw, c);
+  // Chunk order. Without early exit (coop = 0: the first bottom-up level, where hardly any row
+  // is covered) chunks are dealt round robin over the waves, which balances the hubs' expensive
+  // chunks. With early exit a wave takes a contiguous run, so a vertex's later chunks usually
+  // come after its earlier ones have published their bits and are skipped at the first check.
+  // owner[c] = index of chunk c's vertex in wl: one load instead of a ~20-step dependent binary
+  // search over offs.
+  const int64_t cstart = coop ? nchunks * wave / nwaves : wave;
+  const int64_t cend = coop ? nchunks * (wave + 1) / nwaves : nchunks;
+  const int64_t cstep = coop ? 1 : nwaves;
+  for (int64_t c = cstart; c < cend; c += cstep) {
+    const int64_t i = owner[c];
     const int32_t v = wl[i];
     const int64_t j0 = c - (i ? offs[i - 1] : 0);
     const int64_t end = rowptr[v + 1];
@@ -656,9 +695,17 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
         const int64_t e = t0 + q * 64 + lane;
         u[q] = e < lim ? col[e] : -1;
       }
+      if (!(xmode & 2)) {
 #pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (u[q] >= filter_from && !any_visited(anyvis, u[q])) u[q] = -1;
+        for (int q = 0; q < Q; ++q) {
+          bool vis;
+          if (HUBW > 0 && u[q] >= 0 && u[q] < HUBW * 32)
+            vis = (hub[u[q] >> 5] >> (u[q] & 31)) & 1u;
+          else
+            vis = u[q] < filter_from || any_visited(anyvis, u[q]);
+          if (u[q] >= 0 && !vis) u[q] = -1;
+        }
+      }
       int cnt = 0;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
@@ -677,7 +724,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
         }
 #pragma unroll
         for (int q = 0; q < PB; ++q)
-          if (uu[q] >= 0) {
+          if (uu[q] >= 0 && !(xmode & 1)) {
             const V<VW> x = ldv<VW>(R + (int64_t)uu[q] * W + slot * VW);
 #pragma unroll
             for (int j = 0; j < VW; ++j) a.w[j] |= x.w[j];
@@ -720,6 +767,16 @@ __global__ __launch_bounds__(kBlock) void k_bu_chunks(
         if (nb) atomicOr((unsigned long long*)&acc[vo + j], nb);
       }
     }
+  }
+}
+
+// owner[c] = i for every chunk c of wide-list entry i (offs = inclusive chunk-count prefix)
+__global__ __launch_bounds__(kBlock) void k_chunk_owner(const int64_t* offs, int64_t nw,
+                                                        int32_t* owner) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t e = offs[i];
+    for (int64_t c = i ? offs[i - 1] : 0; c < e; ++c) owner[c] = (int32_t)i;
   }
 }
 
@@ -869,10 +926,12 @@ struct WordSplit {
 };
 
 // send[(hi-lo)*wbeg[j] + (v-lo)*nw_j + (w-wbeg[j])] = vis[v*W + w]: destination-major blocks
+// (rows of deg-0 vertices may be stale, see k_zero_src_rows: they are sent as zeros; phase C
+// never reads them either)
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, int64_t lo,
-                                                       int64_t cnt, int wt, WordSplit ws,
-                                                       uint64_t* send) {
+__global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, const int64_t* rowptr,
+                                                       int64_t lo, int64_t cnt, int wt,
+                                                       WordSplit ws, uint64_t* send) {
   const int64_t total = cnt * wt;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
@@ -881,7 +940,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, int6
     int j = 0;
     while (w >= ws.b[j + 1]) ++j;
     const int nw = ws.b[j + 1] - ws.b[j];
-    send[cnt * ws.b[j] + i * nw + (w - ws.b[j])] = vis[(lo + i) * W + w];
+    const bool deg0 = rowptr[lo + i + 1] == rowptr[lo + i];
+    send[cnt * ws.b[j] + i * nw + (w - ws.b[j])] = deg0 ? 0ull : vis[(lo + i) * W + w];
   }
 }
 
@@ -952,7 +1012,7 @@ class BitparSolver final : public Solver {
     {
       size_t free_b = 0, total_b = 0;
       if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
-        const double fixed = 48.0 * (double)n + 64.0 * (1 << 20);
+        const double fixed = 52.0 * (double)n + (double)g.nnz / 256.0 + 64.0 * (1 << 20);
         while (w > 1 && fixed + 32.0 * (double)n * w > 0.92 * (double)free_b) w >>= 1;
         if (fixed + 32.0 * (double)n * w > 0.92 * (double)free_b)
           fail("not enough device memory for the bit-parallel solver (n=" + std::to_string(n) + ")");
@@ -977,6 +1037,7 @@ class BitparSolver final : public Solver {
       fl_[i].alloc((size_t)n * sizeof(int32_t));
     }
     touched_.alloc((size_t)n * sizeof(int32_t));
+    owner_.alloc(((size_t)n + (size_t)(g.nnz / kChunk) + 2) * sizeof(int32_t));  // >= chunks_max
     offs_.alloc((size_t)n * sizeof(int64_t));
     scan_bytes_ = frontier_scan_temp_bytes(n);
     scan_tmp_.alloc(scan_bytes_);
@@ -990,6 +1051,9 @@ class BitparSolver final : public Solver {
     if (const char* d = getenv("MSBFS_DIRS")) dirs_ = d;  // per-level T/B override (tuning)
     if (const char* u = getenv("MSBFS_UNROLL")) unroll_ = atoi(u);
     if (const char* w = getenv("MSBFS_WIDE_LATER")) wide_later_ = atoi(w);
+    if (const char* x = getenv("MSBFS_X")) xmode_ = atoi(x);          // experiments only
+    if (const char* t = getenv("MSBFS_TILE")) tile_ = atoi(t);
+    if (const char* h = getenv("MSBFS_HUBLDS")) hub_lds_ = atoi(h);
     MSBFS_HIP_CHECK(hipDeviceSynchronize());
   }
 
@@ -1149,7 +1213,7 @@ class BitparSolver final : public Solver {
   const DeviceGraph& g_;
   int maxW_ = 1;
   DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
-      ctr_, small_, pairs_, slabF_, slabE_, anyvis_;
+      ctr_, small_, pairs_, slabF_, slabE_, anyvis_, owner_;
   double filter_frac_ = 0.5;  // skip unvisited neighbours while visited edges < frac * nnz
   double hub_bytes_ = 0.0;    // MSBFS_HUB_MB: hub rows loaded without the bitmap test (off: best)
   size_t scan_bytes_ = 0;
@@ -1158,6 +1222,9 @@ class BitparSolver final : public Solver {
   std::string dirs_;
   int unroll_ = 8;
   int wide_later_ = 1024;
+  int xmode_ = 0;
+  int tile_ = 256;
+  int hub_lds_ = 1;
 };
 
 // per-batch reset + sources + level 0 (k_init); leaves the loop state ready for level 1
@@ -1166,8 +1233,7 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
                                Loop& S, hipStream_t s) {
   const int64_t n = g_.n;
   const size_t vb = (size_t)std::max<int64_t>(n, 1) * W * sizeof(uint64_t);
-  MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));
-  MSBFS_HIP_CHECK(hipMemsetAsync(vis_[1].p, 0, vb, s));
+  MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));  // vis_[1]: see k_zero_src_rows
   MSBFS_HIP_CHECK(hipMemsetAsync(done_.p, 0, done_.bytes, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(anyvis_.p, 0, anyvis_.bytes, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
@@ -1202,6 +1268,9 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
   }
   ++epoch_;
   if (np) {
+    k_zero_src_rows<W><<<grid_for(np * W, kBlock), kBlock, 0, s>>>(dpv, np, g_.old2new,
+                                                                  vis_[1].as<uint64_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
     k_init<W, COUNT><<<grid_for(np, kBlock), kBlock, 0, s>>>(
         dpv, dpk, np, g_.rowptr, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
         acc_[S.ac].as<uint64_t>(), stamp_.as<int32_t>(), epoch_, fl_[S.fc].as<int32_t>(),
@@ -1326,10 +1395,25 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         frontier_degree_scan(g_.rowptr, actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(),
                              scan_tmp_.p, scan_bytes_, s, kChunk);
         const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
-        k_bu_chunks<W><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
-            actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
-            sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-            first_bu ? 0 : 1);
+        owner_.ensure((size_t)chunks_max * sizeof(int32_t));
+        k_chunk_owner<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(offs_.as<int64_t>(), S.nactw,
+                                                                   owner_.as<int32_t>());
+        MSBFS_HIP_CHECK(hipGetLastError());
+        constexpr int kHubW = 14336;  // 56 KB of LDS: ids < 458752
+        const bool hub_lds = hub_lds_ && filter_from == 0 && n > (int64_t)kHubW * 32 * 4;
+        if (hub_lds) {
+          k_bu_chunks<W, 256, 1024, kHubW><<<grid_for(chunks_max, 16, 512), 1024, 0, s>>>(
+              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
+              sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
+              first_bu ? 0 : 1, xmode_, owner_.as<int32_t>());
+        } else {
+          auto ck = tile_ >= 1024 ? k_bu_chunks<W, 1024, kBlock, 0>
+                    : tile_ >= 512 ? k_bu_chunks<W, 512, kBlock, 0> : k_bu_chunks<W, 256, kBlock, 0>;
+          ck<<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
+              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
+              sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
+              first_bu ? 0 : 1, xmode_, owner_.as<int32_t>());
+        }
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(S.nactw, L::TILE, grid);
         k_bu_wide_finalize<W, COUNT><<<gw, kBlock, 0, s>>>(
@@ -1429,7 +1513,7 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
     for (int j = 0; j <= nparts; ++j) ws.b[j] = wbeg[j];
     for (int j = nparts + 1; j <= kMaxParts; ++j) ws.b[j] = wt + 1;  // never reached
     k_pack_words<W><<<grid_for((hi - lo) * wt, kBlock, 8192), kBlock, 0, s>>>(
-        vis_[S.cur].as<uint64_t>(), lo, hi - lo, wt, ws, send);
+        vis_[S.cur].as<uint64_t>(), g_.rowptr, lo, hi - lo, wt, ws, send);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   const bool ran_l2 = S.level >= 2;
