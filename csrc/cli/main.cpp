@@ -255,11 +255,13 @@ int main(int argc, char* argv[]) {
 
     // ---- assignment: static round-robin (main.cu:304-307), or whole 64-group words (hybrid)
     std::vector<int32_t> wbeg(P + 1, 0);
-    std::vector<int64_t> bounds(P + 1, 0);
+    std::vector<int64_t> pcount(P, 0);  // vertices of each part (v = part + i*P < n_eff)
+    int64_t n_eff = 0;
     if (hybrid) {
       const int wt = (int)((K + 63) / 64);
       for (int j = 0; j <= P; ++j) wbeg[j] = (int32_t)((int64_t)j * wt / P);
-      hybrid_split(dg, P, 8, bounds.data());
+      n_eff = hybrid_extent(dg);
+      for (int r = 0; r < P; ++r) pcount[r] = n_eff > r ? (n_eff - r + P - 1) / P : 0;
     }
     QuerySet local;
     std::vector<int64_t> local_to_global;
@@ -282,11 +284,11 @@ int main(int argc, char* argv[]) {
     std::vector<int64_t> scount(P, 0), rcount(P, 0), hout, hF;
     const int nw_me = hybrid ? wbeg[me + 1] - wbeg[me] : 0;
     if (hybrid) {
-      const int64_t cnt = bounds[me + 1] - bounds[me];
+      const int64_t cnt = pcount[me];
       int64_t ns = 0, nr = 0;
       for (int j = 0; j < P; ++j) {
         scount[j] = cnt * (wbeg[j + 1] - wbeg[j]);
-        rcount[j] = (bounds[j + 1] - bounds[j]) * nw_me;
+        rcount[j] = pcount[j] * nw_me;
         ns += scount[j];
         nr += rcount[j];
       }
@@ -320,13 +322,13 @@ int main(int argc, char* argv[]) {
       } else if (hybrid) {
         // levels 1-2 vertex-partitioned (all groups), one word all-to-all, the rest per rank
         rs = RunStats();
-        solver->hybrid_phase_a(K, q.off.data(), q.ids.data(), bounds[me], bounds[me + 1], me == 0,
-                               P, wbeg.data(), hsend.as<uint64_t>(), hout.data(), &rs, stream);
+        solver->hybrid_phase_a(K, q.off.data(), q.ids.data(), me, P, n_eff, me == 0, wbeg.data(),
+                               hsend.as<uint64_t>(), hout.data(), &rs, stream);
         comm->alltoallv_device_u64(hsend.as<uint64_t>(), scount, hrecv.as<uint64_t>(), rcount,
                                    stream);
         comm->allreduce_sum_i64(hout.data(), hout.size());
-        solver->hybrid_phase_c(K, wbeg[me], nw_me, hrecv.as<uint64_t>(), hout.data(), hF.data(),
-                               &rs, stream);
+        solver->hybrid_phase_c(K, wbeg[me], nw_me, P, n_eff, hrecv.as<uint64_t>(), hout.data(),
+                               hF.data(), &rs, stream);
         for (int64_t i = 0; i < nlocal; ++i) F[i] = hout[local_to_global[i]] + hF[i];
       } else if (nlocal) {
         rs = RunStats();

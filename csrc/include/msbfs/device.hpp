@@ -119,37 +119,38 @@ class Solver {
                    int64_t* edges2, RunStats* st, hipStream_t stream) = 0;
 
   // ---- hybrid multi-GPU mode (bit-parallel solver only) ------------------------------------
-  // Levels 1-2 run vertex-partitioned (every rank: all K groups, pulls only for vertices in its
-  // range [lo,hi)); one all-to-all hands every rank its own words (groups) for all vertices;
-  // the remaining levels run query-partitioned. See kernels/bitpar.hip "hybrid".
-  // Largest K one hybrid round supports (0: not supported).
+  // Levels 1-2 run vertex-partitioned (every rank: all K groups, pulls only for its residue
+  // class of vertices v = part + i*nparts < n_eff); one all-to-all hands every rank its own
+  // words (groups) for all vertices; the remaining levels run query-partitioned. See
+  // kernels/bitpar.hip "hybrid". Largest K one hybrid round supports (0: not supported).
   virtual int64_t hybrid_max_groups() const { return 0; }
   // Phase A. wbeg[0..nparts]: destination word split (rank j gets words [wbeg[j], wbeg[j+1]) of
-  // ceil(K/64)). send_dev: (hi-lo)*wbeg[nparts] words, destination-major. out_host[2K+3]:
-  // F partial, per-group "new at level 2" flags, then frontier size / edges / visited edges.
-  virtual void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t lo,
-                              int64_t hi, bool count_l1, int nparts, const int32_t* wbeg,
+  // ceil(K/64)). send_dev: cnt*wbeg[nparts] words, destination-major, cnt = own vertices.
+  // out_host[2K+3]: F partial, per-group "new at level 2" flags, then frontier size / edges /
+  // visited edges.
+  virtual void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part,
+                              int nparts, int64_t n_eff, bool count_l1, const int32_t* wbeg,
                               uint64_t* send_dev, int64_t* out_host, RunStats* st,
                               hipStream_t stream) {
-    (void)K, (void)qoff, (void)qids, (void)lo, (void)hi, (void)count_l1, (void)nparts,
+    (void)K, (void)qoff, (void)qids, (void)part, (void)nparts, (void)n_eff, (void)count_l1,
         (void)wbeg, (void)send_dev, (void)out_host, (void)st, (void)stream;
     fail("this solver has no hybrid mode (use the bit-parallel solver)");
   }
-  // Phase C. recv_dev: n*w_count words (this rank's words of every vertex, vertex-major);
+  // Phase C. recv_dev: for every source part r in order, w_count words of each of r's vertices;
   // reduced[2K+3]: out_host summed over ranks. F_out[64*w_count] (local groups): levels >= 3.
-  virtual void hybrid_phase_c(int64_t K, int w_begin, int w_count, const uint64_t* recv_dev,
-                              const int64_t* reduced, int64_t* F_out, RunStats* st,
-                              hipStream_t stream) {
-    (void)K, (void)w_begin, (void)w_count, (void)recv_dev, (void)reduced, (void)F_out, (void)st,
-        (void)stream;
+  virtual void hybrid_phase_c(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
+                              const uint64_t* recv_dev, const int64_t* reduced, int64_t* F_out,
+                              RunStats* st, hipStream_t stream) {
+    (void)K, (void)w_begin, (void)w_count, (void)nparts, (void)n_eff, (void)recv_dev,
+        (void)reduced, (void)F_out, (void)st, (void)stream;
     fail("this solver has no hybrid mode (use the bit-parallel solver)");
   }
   SolverOptions opt;
 };
 
-// Vertex ranges for the hybrid mode: bounds[0..nparts] with bounds[0]=0, bounds[nparts]=n,
-// balanced on deg(v) + vertex_weight (edges dominate the pull cost, vertices the exchange).
-void hybrid_split(const DeviceGraph& g, int nparts, int64_t vertex_weight, int64_t* bounds);
+// Vertices taking part in the hybrid exchange: 1 + the last vertex with deg > 0 (after degree
+// relabelling every isolated vertex is in the suffix [n_eff, n)).
+int64_t hybrid_extent(const DeviceGraph& g);
 
 std::unique_ptr<Solver> make_bitpar_solver(const DeviceGraph& g, int max_groups);
 std::unique_ptr<Solver> make_dist_solver(const DeviceGraph& g);

@@ -102,23 +102,24 @@ int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32
 void msbfs_solver_free(msbfs_solver s);
 
 /* ---- hybrid multi-GPU mode (bit-parallel solver) ----
- * Levels 1-2 vertex-partitioned (each rank: all K groups, bottom-up pulls only for its vertex
- * range), one all-to-all of visited words, remaining levels query-partitioned (rank j owns the
- * groups of words [wbeg[j], wbeg[j+1]) of ceil(K/64)). The caller does the communication:
- *   A: phase_a -> send_dev (device, (hi-lo)*ceil(K/64) u64, destination-major), out[2K+3]
- *   exchange: all-to-all send -> recv (rank j receives n*(wbeg[j+1]-wbeg[j]) u64 in vertex
- *             order), all-reduce SUM of out -> reduced
+ * Levels 1-2 vertex-partitioned (each rank: all K groups, bottom-up pulls only for its vertices
+ * v = part + i*nparts < n_eff), one all-to-all of visited words, remaining levels
+ * query-partitioned (rank j owns the groups of words [wbeg[j], wbeg[j+1]) of ceil(K/64)). The
+ * caller does the communication (cnt_r = number of vertices of part r):
+ *   A: phase_a -> send_dev (device, cnt_me*ceil(K/64) u64, destination-major), out[2K+3]
+ *   exchange: all-to-all send -> recv (rank j receives cnt_r*(wbeg[j+1]-wbeg[j]) u64 from each
+ *             rank r, in rank order), all-reduce SUM of out -> reduced
  *   C: phase_c(recv, reduced) -> F_local[64*nwords] (levels >= 3 of the own groups)
  *   F[k] = reduced[k] + F_local[k - 64*wbeg[rank]] for the own groups. */
-int msbfs_hybrid_split(msbfs_graph g, int nparts, int64_t vertex_weight, int64_t* bounds);
+int msbfs_hybrid_extent(msbfs_graph g, int64_t* n_eff);
 int64_t msbfs_solver_hybrid_max_groups(msbfs_solver s);
 int msbfs_solver_hybrid_phase_a(msbfs_solver s, int64_t K, const int64_t* qoff,
-                                const int32_t* qids, int64_t lo, int64_t hi, int count_l1,
-                                int nparts, const int32_t* wbeg, void* send_dev, int64_t* out,
+                                const int32_t* qids, int part, int nparts, int64_t n_eff,
+                                int count_l1, const int32_t* wbeg, void* send_dev, int64_t* out,
                                 msbfs_stats* st, void* stream);
-int msbfs_solver_hybrid_phase_c(msbfs_solver s, int64_t K, int w_begin, int w_count,
-                                const void* recv_dev, const int64_t* reduced, int64_t* F_local,
-                                msbfs_stats* st, void* stream);
+int msbfs_solver_hybrid_phase_c(msbfs_solver s, int64_t K, int w_begin, int w_count, int nparts,
+                                int64_t n_eff, const void* recv_dev, const int64_t* reduced,
+                                int64_t* F_local, msbfs_stats* st, void* stream);
 
 /* reference argmin (main.cu:381-397): first valid, strict '<', lowest index wins ties; -1 if K=0 */
 int64_t msbfs_argmin(const int64_t* F, int64_t K);

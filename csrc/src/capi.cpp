@@ -382,8 +382,8 @@ int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32
   });
 }
 
-int msbfs_hybrid_split(msbfs_graph g, int nparts, int64_t vertex_weight, int64_t* bounds) {
-  return guard([&] { msbfs::hybrid_split(g->g, nparts, vertex_weight, bounds); });
+int msbfs_hybrid_extent(msbfs_graph g, int64_t* n_eff) {
+  return guard([&] { *n_eff = msbfs::hybrid_extent(g->g); });
 }
 
 int64_t msbfs_solver_hybrid_max_groups(msbfs_solver s) {
@@ -391,24 +391,24 @@ int64_t msbfs_solver_hybrid_max_groups(msbfs_solver s) {
 }
 
 int msbfs_solver_hybrid_phase_a(msbfs_solver s, int64_t K, const int64_t* qoff,
-                                const int32_t* qids, int64_t lo, int64_t hi, int count_l1,
-                                int nparts, const int32_t* wbeg, void* send_dev, int64_t* out,
+                                const int32_t* qids, int part, int nparts, int64_t n_eff,
+                                int count_l1, const int32_t* wbeg, void* send_dev, int64_t* out,
                                 msbfs_stats* st, void* stream) {
   return guard([&] {
     timed(s, stream, st, [&](msbfs::RunStats* rs, hipStream_t hs) {
-      s->impl->hybrid_phase_a(K, qoff, qids, lo, hi, count_l1 != 0, nparts, wbeg,
+      s->impl->hybrid_phase_a(K, qoff, qids, part, nparts, n_eff, count_l1 != 0, wbeg,
                               (uint64_t*)send_dev, out, rs, hs);
     });
   });
 }
 
-int msbfs_solver_hybrid_phase_c(msbfs_solver s, int64_t K, int w_begin, int w_count,
-                                const void* recv_dev, const int64_t* reduced, int64_t* F_local,
-                                msbfs_stats* st, void* stream) {
+int msbfs_solver_hybrid_phase_c(msbfs_solver s, int64_t K, int w_begin, int w_count, int nparts,
+                                int64_t n_eff, const void* recv_dev, const int64_t* reduced,
+                                int64_t* F_local, msbfs_stats* st, void* stream) {
   return guard([&] {
     timed(s, stream, st, [&](msbfs::RunStats* rs, hipStream_t hs) {
-      s->impl->hybrid_phase_c(K, w_begin, w_count, (const uint64_t*)recv_dev, reduced, F_local,
-                              rs, hs);
+      s->impl->hybrid_phase_c(K, w_begin, w_count, nparts, n_eff, (const uint64_t*)recv_dev,
+                              reduced, F_local, rs, hs);
     });
   });
 }

@@ -259,11 +259,13 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
 // buffers are valid wherever a kernel looks. Saves one n*W*8-byte fill per batch.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_zero_src_rows(const int32_t* pv, int64_t np,
-                                                         const int32_t* relabel, uint64_t* visB) {
+                                                         const int32_t* relabel, uint64_t* visA,
+                                                         uint64_t* visB) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < np * W;
        i += (int64_t)gridDim.x * kBlock) {
     int32_t v = pv[i / W];
     if (relabel) v = relabel[v];
+    visA[(int64_t)v * W + (i % W)] = 0;
     visB[(int64_t)v * W + (i % W)] = 0;
   }
 }
@@ -461,9 +463,10 @@ __global__ __launch_bounds__(kBlock) void k_zero_acc(const int32_t* fl, int64_t 
   }
 }
 
-// build the bottom-up active lists (deg > 0, not done) over the vertex range [lo, hi), split
-// by degree (the hybrid mode's vertex-partitioned level pulls only for its own range)
-__global__ __launch_bounds__(kBlock) void k_build_active(int64_t lo, int64_t hi,
+// build the bottom-up active lists (deg > 0, not done) over the vertices v = part + i*nparts,
+// i < cnt, split by degree (nparts = 1: every vertex; the hybrid mode's vertex-partitioned
+// level pulls only for its own residue class)
+__global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, int nparts,
                                                          const int64_t* rowptr,
                                                          const uint32_t* done, int wide_deg,
                                                          int32_t* act, int32_t* actw, Ctr* ctr) {
@@ -473,11 +476,12 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t lo, int64_t hi,
   q_init(qw);
   __syncthreads();
   unsigned long long eu = 0;
-  for (int64_t b = lo + (int64_t)blockIdx.x * kBlock; b < hi; b += (int64_t)gridDim.x * kBlock) {
-    const int64_t i = b + threadIdx.x;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < cnt; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t j = b + threadIdx.x;
+    const int64_t i = part + j * nparts;
     int64_t d = 0;
     bool ok = false;
-    if (i < hi) {
+    if (j < cnt) {
       d = rowptr[i + 1] - rowptr[i];
       ok = d > 0 && !is_done(done, (int32_t)i);
     }
@@ -916,40 +920,49 @@ __global__ __launch_bounds__(kBlock) void k_count_frontier(const int32_t* fl, co
 // graph at the first bottom-up level, whose cost hardly depends on the number of groups (a row
 // scan stops only once EVERY group is covered), so 8 GPUs each pay most of one GPU's time. Levels
 // 1-2 need only the sources' neighbourhoods, which every rank can build for all groups, so level
-// 2 is split by vertex range (each rank pulls 1/N of the edges for all groups) and one
-// all-to-all then gives every rank its own block of words for every vertex (hybrid 2D
-// decomposition: vertex-partitioned for the explosive level, query-partitioned after it).
+// 2 is split by vertex (each rank pulls for its residue class v = part mod nparts, for all
+// groups) and one all-to-all then gives every rank its own block of words for every vertex
+// (hybrid 2D decomposition: vertex-partitioned for the explosive level, query-partitioned after
+// it). The cyclic vertex split balances both the pull work (hubs and tail spread evenly) and the
+// exchange (every rank sends the same number of rows); vertices >= n_eff (the deg-0 suffix of a
+// degree-relabelled graph) are not exchanged at all.
 // ---------------------------------------------------------------------------------------------
 constexpr int kMaxParts = 64;
 struct WordSplit {
   int32_t b[kMaxParts + 1];
 };
+struct PartPrefix {
+  int64_t b[kMaxParts + 1];  // b[r] = number of vertices owned by parts < r
+};
 
-// send[(hi-lo)*wbeg[j] + (v-lo)*nw_j + (w-wbeg[j])] = vis[v*W + w]: destination-major blocks
+// send[cnt*wbeg[j] + i*nw_j + (w-wbeg[j])] = vis[v*W + w], v = part + i*nparts: destination-major
 // (rows of deg-0 vertices may be stale, see k_zero_src_rows: they are sent as zeros; phase C
 // never reads them either)
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, const int64_t* rowptr,
-                                                       int64_t lo, int64_t cnt, int wt,
+                                                       int part, int nparts, int64_t cnt, int wt,
                                                        WordSplit ws, uint64_t* send) {
   const int64_t total = cnt * wt;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
     const int64_t i = t / wt;
     const int w = (int)(t - i * wt);
+    const int64_t v = part + i * nparts;
     int j = 0;
     while (w >= ws.b[j + 1]) ++j;
     const int nw = ws.b[j + 1] - ws.b[j];
-    const bool deg0 = rowptr[lo + i + 1] == rowptr[lo + i];
-    send[cnt * ws.b[j] + i * nw + (w - ws.b[j])] = deg0 ? 0ull : vis[(lo + i) * W + w];
+    const bool deg0 = rowptr[v + 1] == rowptr[v];
+    send[cnt * ws.b[j] + i * nw + (w - ws.b[j])] = deg0 ? 0ull : vis[v * W + w];
   }
 }
 
 // Phase C state from the received words: both visited buffers (stride W, zero padding beyond
 // nw), done = every alive group present, anyvis = any bit. One thread per vertex; the bitmaps
 // are written with plain stores from wave ballots (64 vertices = 2 words), so no memset.
+// recv holds, per source part r (in order), nw words of each of r's vertices v = r + i*nparts.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, int nw, int64_t n,
+                                                         int64_t n_eff, int nparts, PartPrefix pre,
                                                          uint64_t* visA, uint64_t* visB,
                                                          const uint64_t* alive,
                                                          const uint64_t* gmask, uint32_t* done,
@@ -963,9 +976,11 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
     bool full = false, nz = false;
     if (v < n) {
       full = true;
+      const uint64_t* src = nullptr;
+      if (v < n_eff) src = recv + (pre.b[v % nparts] + v / nparts) * nw;
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        const uint64_t x = w < nw ? recv[v * nw + w] : 0ull;
+        const uint64_t x = (src && w < nw) ? src[w] : 0ull;
         visA[v * W + w] = x;
         visB[v * W + w] = x;
         nz |= x != 0;
@@ -982,20 +997,11 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
   }
 }
 
-// bounds[p] = first v with rowptr[v] + vw*v >= p/nparts of the total (bounds[0]=0, [nparts]=n)
-__global__ void k_split_bounds(const int64_t* rowptr, int64_t n, int nparts, int64_t vw,
-                               int64_t* bounds) {
-  const int p = (int)threadIdx.x;
-  if (p > nparts) return;
-  const int64_t total = rowptr[n] + vw * n;
-  const int64_t target = total / nparts * p + total % nparts * p / nparts;
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (rowptr[mid] + vw * mid >= target) hi = mid;
-    else lo = mid + 1;
-  }
-  bounds[p] = p == 0 ? 0 : (p == nparts ? n : lo);
+// n_eff = 1 + the last vertex with deg > 0 (0 if none)
+__global__ void k_extent(const int64_t* rowptr, int64_t n, unsigned long long* out) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+       v += (int64_t)gridDim.x * blockDim.x)
+    if (rowptr[v + 1] > rowptr[v]) atomicMax(out, (unsigned long long)(v + 1));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1073,14 +1079,15 @@ class BitparSolver final : public Solver {
 
   int64_t hybrid_max_groups() const override { return 64 * (int64_t)maxW_; }
 
-  void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t lo, int64_t hi,
-                      bool count_l1, int nparts, const int32_t* wbeg, uint64_t* send,
+  void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,
+                      int64_t n_eff, bool count_l1, const int32_t* wbeg, uint64_t* send,
                       int64_t* out, RunStats* st, hipStream_t s) override {
     if (K < 1 || K > hybrid_max_groups())
       fail("hybrid mode: K=" + std::to_string(K) + " groups exceeds one round (" +
            std::to_string(hybrid_max_groups()) + ")");
-    if (lo < 0 || hi < lo || hi > g_.n) fail("hybrid mode: bad vertex range");
     if (nparts < 1 || nparts > kMaxParts) fail("hybrid mode: 1..64 ranks");
+    if (part < 0 || part >= nparts) fail("hybrid mode: bad part index");
+    if (n_eff < this->n_eff() || n_eff > g_.n) fail("hybrid mode: bad vertex extent");
     const int wt = (int)((K + 63) / 64);
     if (wbeg[0] != 0 || wbeg[nparts] != wt) fail("hybrid mode: word split must cover ceil(K/64)");
     for (int j = 0; j < nparts; ++j)
@@ -1089,7 +1096,7 @@ class BitparSolver final : public Solver {
     while (w < wt) w <<= 1;
 #define MSBFS_BP_CASE(WW)                                                                  \
   case WW:                                                                                 \
-    phase_a_impl<WW>(K, qoff, qids, lo, hi, count_l1, nparts, wbeg, send, out, st, s);     \
+    phase_a_impl<WW>(K, qoff, qids, part, nparts, n_eff, count_l1, wbeg, send, out, st, s); \
     break;
     switch (w) {
       MSBFS_BP_CASE(1)
@@ -1103,17 +1110,19 @@ class BitparSolver final : public Solver {
     if (st) st->batches++;
   }
 
-  void hybrid_phase_c(int64_t K, int w_begin, int w_count, const uint64_t* recv,
-                      const int64_t* reduced, int64_t* F_out, RunStats* st,
+  void hybrid_phase_c(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
+                      const uint64_t* recv, const int64_t* reduced, int64_t* F_out, RunStats* st,
                       hipStream_t s) override {
     if (w_count <= 0) return;
     if (w_begin < 0 || (int64_t)(w_begin + w_count) * 64 - 63 > K || w_count > maxW_)
       fail("hybrid mode: bad word block");
+    if (nparts < 1 || nparts > kMaxParts) fail("hybrid mode: 1..64 ranks");
+    if (n_eff < this->n_eff() || n_eff > g_.n) fail("hybrid mode: bad vertex extent");
     int w = 1;
     while (w < w_count) w <<= 1;
-#define MSBFS_BP_CASE(WW)                                                          \
-  case WW:                                                                         \
-    phase_c_impl<WW>(K, w_begin, w_count, recv, reduced, F_out, st, s);            \
+#define MSBFS_BP_CASE(WW)                                                               \
+  case WW:                                                                              \
+    phase_c_impl<WW>(K, w_begin, w_count, nparts, n_eff, recv, reduced, F_out, st, s);  \
     break;
     switch (w) {
       MSBFS_BP_CASE(1)
@@ -1140,7 +1149,8 @@ class BitparSolver final : public Solver {
     int bu_levels = 0;
     // limits
     uint32_t stop_level = 0xFFFFFFFFu;  // last level to run
-    int64_t lo = 0, hi = 0;             // vertex range of the first active-list build
+    int64_t cnt = 0;                    // first active-list build: v = part + i*nparts, i < cnt
+    int part = 0, nparts = 1;
     bool weight_l1 = true;              // add level-1 counts to F
     std::string plan;                   // plan[level] = 'T'/'B' forces the next level
     int64_t ev_l1 = 0;                  // ev after level 1
@@ -1170,12 +1180,13 @@ class BitparSolver final : public Solver {
   void batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids, int64_t* F,
                   int64_t* edges2, RunStats* st, hipStream_t s);
   template <int W>
-  void phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t lo, int64_t hi,
-                    bool count_l1, int nparts, const int32_t* wbeg, uint64_t* send, int64_t* out,
-                    RunStats* st, hipStream_t s);
+  void phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,
+                    int64_t n_eff, bool count_l1, const int32_t* wbeg, uint64_t* send,
+                    int64_t* out, RunStats* st, hipStream_t s);
   template <int W>
-  void phase_c_impl(int64_t K, int w_begin, int w_count, const uint64_t* recv,
-                    const int64_t* reduced, int64_t* F_out, RunStats* st, hipStream_t s);
+  void phase_c_impl(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
+                    const uint64_t* recv, const int64_t* reduced, int64_t* F_out, RunStats* st,
+                    hipStream_t s);
 
   void run_batch(int w, int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
                  int64_t* F, int64_t* edges2, RunStats* st, hipStream_t s) {
@@ -1194,6 +1205,19 @@ class BitparSolver final : public Solver {
       default: fail("bad word count");
     }
 #undef MSBFS_BP_CASE
+  }
+
+  // 1 + the last vertex with deg > 0 (cached per graph buffers: relabelling replaces them).
+  // Vertices beyond it are never active, never neighbours: level loops and clears skip them.
+  int64_t n_eff() {
+    if (eff_key_[0] != (const void*)g_.rowptr || eff_key_[1] != (const void*)g_.col ||
+        eff_key_[2] != (const void*)g_.old2new) {
+      n_eff_ = hybrid_extent(g_);
+      eff_key_[0] = g_.rowptr;
+      eff_key_[1] = g_.col;
+      eff_key_[2] = g_.old2new;
+    }
+    return n_eff_;
   }
 
   HostCtr read_ctr(hipStream_t s) {
@@ -1225,6 +1249,8 @@ class BitparSolver final : public Solver {
   int xmode_ = 0;
   int tile_ = 256;
   int hub_lds_ = 1;
+  int64_t n_eff_ = 0;
+  const void* eff_key_[3] = {nullptr, nullptr, nullptr};
 };
 
 // per-batch reset + sources + level 0 (k_init); leaves the loop state ready for level 1
@@ -1232,8 +1258,10 @@ template <int W, bool COUNT>
 void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
                                Loop& S, hipStream_t s) {
   const int64_t n = g_.n;
-  const size_t vb = (size_t)std::max<int64_t>(n, 1) * W * sizeof(uint64_t);
-  MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));  // vis_[1]: see k_zero_src_rows
+  // Rows of vertices >= n_eff (deg 0) are never read: only sources can be there, and their rows
+  // are zeroed by k_zero_src_rows. vis_[1]: see k_zero_src_rows.
+  const size_t vb = (size_t)std::max<int64_t>(n_eff(), 1) * W * sizeof(uint64_t);
+  MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(done_.p, 0, done_.bytes, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(anyvis_.p, 0, anyvis_.bytes, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
@@ -1268,8 +1296,8 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
   }
   ++epoch_;
   if (np) {
-    k_zero_src_rows<W><<<grid_for(np * W, kBlock), kBlock, 0, s>>>(dpv, np, g_.old2new,
-                                                                  vis_[1].as<uint64_t>());
+    k_zero_src_rows<W><<<grid_for(np * W, kBlock), kBlock, 0, s>>>(
+        dpv, np, g_.old2new, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>());
     MSBFS_HIP_CHECK(hipGetLastError());
     k_init<W, COUNT><<<grid_for(np, kBlock), kBlock, 0, s>>>(
         dpv, dpk, np, g_.rowptr, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
@@ -1357,8 +1385,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
         // off only for much higher degrees, so later lists are split at a higher threshold
         const int wide0 = S.bu_levels == 0 ? opt.wide_degree : next_wide;
-        k_build_active<<<grid_for(S.hi - S.lo, kBlock), kBlock, 0, s>>>(
-            S.lo, S.hi, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
+        k_build_active<<<grid_for(S.cnt, kBlock), kBlock, 0, s>>>(
+            S.cnt, S.part, S.nparts, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
             actw_[0].as<int32_t>(), ctr_.as<Ctr>());
         MSBFS_HIP_CHECK(hipGetLastError());
         c = read_ctr(s);
@@ -1476,8 +1504,7 @@ template <int W, bool COUNT>
 void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
                               int64_t* Fout, int64_t* edges2, RunStats* st, hipStream_t s) {
   Loop S;
-  S.lo = 0;
-  S.hi = g_.n;
+  S.cnt = n_eff();
   start_batch<W, COUNT>(k0, nb, qoff, qids, S, s);
   levels<W, COUNT>(S, st, s);
   // frontier is empty: accumulator entries were cleared by finalize / zero_acc
@@ -1488,15 +1515,21 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
   }
 }
 
+// own vertices of part `part` of `nparts` below n_eff: v = part + i*nparts
+static inline int64_t part_count(int64_t n_eff, int part, int nparts) {
+  return n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
+}
+
 // Phase A: level 1 (top-down, every rank identical, only rank 0 adds it to F), level 2
-// (bottom-up over this rank's vertex range only), then pack this range's words per destination.
+// (bottom-up over this rank's residue class only), then pack its rows' words per destination.
 template <int W>
-void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t lo,
-                                int64_t hi, bool count_l1, int nparts, const int32_t* wbeg,
+void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int part,
+                                int nparts, int64_t n_eff, bool count_l1, const int32_t* wbeg,
                                 uint64_t* send, int64_t* out, RunStats* st, hipStream_t s) {
   Loop S;
-  S.lo = lo;
-  S.hi = hi;
+  S.part = part;
+  S.nparts = nparts;
+  S.cnt = part_count(n_eff, part, nparts);
   S.stop_level = 2;
   S.weight_l1 = count_l1;
   S.plan = "TB";
@@ -1508,12 +1541,12 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   const int wt = (int)((K + 63) / 64);
-  if (hi > lo) {
+  if (S.cnt > 0) {
     WordSplit ws{};
     for (int j = 0; j <= nparts; ++j) ws.b[j] = wbeg[j];
     for (int j = nparts + 1; j <= kMaxParts; ++j) ws.b[j] = wt + 1;  // never reached
-    k_pack_words<W><<<grid_for((hi - lo) * wt, kBlock, 8192), kBlock, 0, s>>>(
-        vis_[S.cur].as<uint64_t>(), g_.rowptr, lo, hi - lo, wt, ws, send);
+    k_pack_words<W><<<grid_for(S.cnt * wt, kBlock, 8192), kBlock, 0, s>>>(
+        vis_[S.cur].as<uint64_t>(), g_.rowptr, part, nparts, S.cnt, wt, ws, send);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   const bool ran_l2 = S.level >= 2;
@@ -1532,9 +1565,9 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
 // Phase C: rebuild the level-2 state of this rank's groups from the exchanged words and run
 // the remaining levels (the first one bottom-up: the frontier is only implicit in the words).
 template <int W>
-void BitparSolver::phase_c_impl(int64_t K, int w_begin, int w_count, const uint64_t* recv,
-                                const int64_t* reduced, int64_t* F_out, RunStats* st,
-                                hipStream_t s) {
+void BitparSolver::phase_c_impl(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
+                                const uint64_t* recv, const int64_t* reduced, int64_t* F_out,
+                                RunStats* st, hipStream_t s) {
   const int64_t n = g_.n;
   MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
   MSBFS_HIP_CHECK(hipMemsetAsync(small_.p, 0, small_.bytes, s));
@@ -1552,15 +1585,16 @@ void BitparSolver::phase_c_impl(int64_t K, int w_begin, int w_count, const uint6
     MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, ha[1], sizeof(ha[1]), hipMemcpyHostToDevice, s));
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
   }
-  if (n > 0) {
-    k_hybrid_setup<W><<<grid_for(n, kBlock, 8192), kBlock, 0, s>>>(
-        recv, w_count, n, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(), sm.alive[0], sm.gmask,
-        done_.as<uint32_t>(), anyvis_.as<uint32_t>());
+  if (n_eff > 0) {  // vertices >= n_eff have no edges: no kernel reads their rows or bits
+    PartPrefix pre{};
+    for (int r = 0; r < nparts; ++r) pre.b[r + 1] = pre.b[r] + part_count(n_eff, r, nparts);
+    k_hybrid_setup<W><<<grid_for(n_eff, kBlock, 8192), kBlock, 0, s>>>(
+        recv, w_count, n_eff, n_eff, nparts, pre, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
+        sm.alive[0], sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>());
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   Loop S;
-  S.lo = 0;
-  S.hi = n;
+  S.cnt = n_eff;
   S.level = 2;
   S.nf = reduced[2 * K];
   S.ef = reduced[2 * K + 1];
@@ -1582,16 +1616,17 @@ std::unique_ptr<Solver> make_bitpar_solver(const DeviceGraph& g, int max_groups)
   return std::make_unique<bp::BitparSolver>(g, max_groups);
 }
 
-void hybrid_split(const DeviceGraph& g, int nparts, int64_t vertex_weight, int64_t* bounds) {
-  if (nparts < 1 || nparts > 1023) fail("hybrid_split: 1..1023 parts");
-  if (vertex_weight < 0) fail("hybrid_split: negative vertex weight");
+int64_t hybrid_extent(const DeviceGraph& g) {
   MSBFS_HIP_CHECK(hipSetDevice(g.device));
+  if (g.n <= 0) return 0;
   DevBuf d;
-  d.alloc((size_t)(nparts + 1) * sizeof(int64_t));
-  bp::k_split_bounds<<<1, 1024>>>(g.rowptr, g.n, nparts, vertex_weight, d.as<int64_t>());
+  d.alloc(sizeof(unsigned long long));
+  MSBFS_HIP_CHECK(hipMemset(d.p, 0, sizeof(unsigned long long)));
+  bp::k_extent<<<grid_for(g.n, 256, 8192), 256>>>(g.rowptr, g.n, d.as<unsigned long long>());
   MSBFS_HIP_CHECK(hipGetLastError());
-  MSBFS_HIP_CHECK(hipMemcpy(bounds, d.p, (size_t)(nparts + 1) * sizeof(int64_t),
-                            hipMemcpyDeviceToHost));
+  unsigned long long h = 0;
+  MSBFS_HIP_CHECK(hipMemcpy(&h, d.p, sizeof(h), hipMemcpyDeviceToHost));
+  return (int64_t)h;
 }
 
 }  // namespace msbfs

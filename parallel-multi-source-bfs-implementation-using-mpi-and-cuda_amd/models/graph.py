@@ -213,12 +213,12 @@ class DeviceGraph:
         native.check(native.lib().msbfs_graph_relabel_map(self.handle, native.ptr(out, C.c_int32)))
         return out
 
-    def hybrid_split(self, nparts: int, vertex_weight: int = 8) -> np.ndarray:
-        """Vertex range bounds[0..nparts] balanced on deg(v) + vertex_weight (hybrid mode)."""
-        b = np.zeros(nparts + 1, dtype=np.int64)
-        native.check(native.lib().msbfs_hybrid_split(self.handle, int(nparts), int(vertex_weight),
-                                                     native.ptr(b, C.c_int64)))
-        return b
+    def hybrid_extent(self) -> int:
+        """1 + the last vertex with deg > 0: the vertices the hybrid mode exchanges (after degree
+        relabelling the isolated vertices form the suffix [extent, n))."""
+        out = np.zeros(1, dtype=np.int64)
+        native.check(native.lib().msbfs_hybrid_extent(self.handle, native.ptr(out, C.c_int64)))
+        return int(out[0])
 
     def download(self) -> Graph:
         rowptr = np.empty(self.n + 1, dtype=np.int64)

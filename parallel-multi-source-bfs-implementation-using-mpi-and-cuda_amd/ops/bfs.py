@@ -67,34 +67,37 @@ class Solver:
     def hybrid_max_groups(self) -> int:
         return int(native.lib().msbfs_solver_hybrid_max_groups(self._h))
 
-    def hybrid_phase_a(self, queries: QuerySet, lo: int, hi: int, count_l1: bool,
-                       wbeg: np.ndarray, send_ptr: int, stream: Optional[int] = None):
-        """Levels 1-2 of all groups, level-2 pulls for vertices [lo, hi) only; packs this
-        range's visited words into the device buffer at send_ptr. Returns (out[2K+3], stats)."""
+    def hybrid_phase_a(self, queries: QuerySet, part: int, nparts: int, n_eff: int,
+                       count_l1: bool, wbeg: np.ndarray, send_ptr: int,
+                       stream: Optional[int] = None):
+        """Levels 1-2 of all groups, level-2 pulls only for the vertices v = part + i*nparts
+        below n_eff; packs their visited words into the device buffer at send_ptr (destination-
+        major). Returns (out[2K+3], stats)."""
         K = queries.K
         wbeg = np.ascontiguousarray(wbeg, dtype=np.int32)
         out = np.zeros(2 * K + 3, dtype=np.int64)
         st = native.Stats()
         native.check(native.lib().msbfs_solver_hybrid_phase_a(
             self._h, K, native.ptr(queries.off, C.c_int64), native.ptr(queries.ids, C.c_int32),
-            int(lo), int(hi), int(bool(count_l1)), len(wbeg) - 1, native.ptr(wbeg, C.c_int32),
+            int(part), int(nparts), int(n_eff), int(bool(count_l1)), native.ptr(wbeg, C.c_int32),
             C.c_void_p(send_ptr), native.ptr(out, C.c_int64), C.byref(st),
             C.c_void_p(stream) if stream else None))
         return out, st.as_dict()
 
-    def hybrid_phase_c(self, K: int, w_begin: int, w_count: int, recv_ptr: int,
-                       reduced: np.ndarray, stream: Optional[int] = None):
+    def hybrid_phase_c(self, K: int, w_begin: int, w_count: int, nparts: int, n_eff: int,
+                       recv_ptr: int, reduced: np.ndarray, stream: Optional[int] = None):
         """Levels >= 3 of the groups in words [w_begin, w_begin + w_count) from the exchanged
-        words at recv_ptr (n * w_count u64). Returns (F_local[64 * w_count], stats)."""
+        words at recv_ptr (per source part, w_count u64 of each of its vertices). Returns
+        (F_local[64 * w_count], stats)."""
         reduced = np.ascontiguousarray(reduced, dtype=np.int64)
         if len(reduced) != 2 * K + 3:
             raise ValueError("reduced must have 2K+3 entries")
         F = np.zeros(max(1, 64 * w_count), dtype=np.int64)
         st = native.Stats()
         native.check(native.lib().msbfs_solver_hybrid_phase_c(
-            self._h, int(K), int(w_begin), int(w_count), C.c_void_p(recv_ptr),
-            native.ptr(reduced, C.c_int64), native.ptr(F, C.c_int64), C.byref(st),
-            C.c_void_p(stream) if stream else None))
+            self._h, int(K), int(w_begin), int(w_count), int(nparts), int(n_eff),
+            C.c_void_p(recv_ptr), native.ptr(reduced, C.c_int64), native.ptr(F, C.c_int64),
+            C.byref(st), C.c_void_p(stream) if stream else None))
         return F, st.as_dict()
 
     def close(self) -> None:

@@ -88,12 +88,13 @@ def _sig(lib):
         "msbfs_solver_run": (C.c_int, [vp, C.c_int64, i64p, i32p, i64p, i64p, P(Stats), vp]),
         "msbfs_solver_free": (None, [vp]),
         "msbfs_argmin": (C.c_int64, [i64p, C.c_int64]),
-        "msbfs_hybrid_split": (C.c_int, [vp, C.c_int, C.c_int64, i64p]),
+        "msbfs_hybrid_extent": (C.c_int, [vp, i64p]),
         "msbfs_solver_hybrid_max_groups": (C.c_int64, [vp]),
-        "msbfs_solver_hybrid_phase_a": (C.c_int, [vp, C.c_int64, i64p, i32p, C.c_int64, C.c_int64,
-                                                  C.c_int, C.c_int, i32p, vp, i64p, P(Stats), vp]),
-        "msbfs_solver_hybrid_phase_c": (C.c_int, [vp, C.c_int64, C.c_int, C.c_int, vp, i64p, i64p,
-                                                  P(Stats), vp]),
+        "msbfs_solver_hybrid_phase_a": (C.c_int, [vp, C.c_int64, i64p, i32p, C.c_int, C.c_int,
+                                                  C.c_int64, C.c_int, i32p, vp, i64p, P(Stats),
+                                                  vp]),
+        "msbfs_solver_hybrid_phase_c": (C.c_int, [vp, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                                  C.c_int64, vp, i64p, i64p, P(Stats), vp]),
     }
     for name, (res, args) in specs.items():
         f = getattr(lib, name)

@@ -5,12 +5,16 @@ Reference: the only decomposition in main.cu is static round-robin over query gr
 keeps the replica but changes the split:
 
   phase A  every rank runs levels 1-2 for ALL groups (<= 1024, one pass), but the level-2
-           bottom-up pull only for its own edge-balanced vertex range. Level 2 is the explosive
-           level: its row scans cost nearly the same for 128 groups as for 1024 (a scan stops
-           only when every group is covered), so round-robin makes all N GPUs pay ~all of it.
-  exchange one all-to-all of 64-bit visited words: rank j receives, for every vertex, the
-           words of its own group block (1/N of the words); plus one small SUM all-reduce of
-           the phase-A partial sums, "still alive" flags and frontier sizes.
+           bottom-up pull only for its own vertices v = rank + i*world (cyclic split: hubs and
+           tail spread evenly, so pull work AND exchange volume are balanced). Level 2 is the
+           explosive level: its row scans cost nearly the same for 128 groups as for 1024 (a
+           scan stops only when every group is covered), so round-robin makes all N GPUs pay
+           ~all of it.
+  exchange one all-to-all of 64-bit visited words: rank j receives, for every vertex below
+           n_eff (= 1 + the last vertex with an edge; a degree-relabelled graph keeps its
+           isolated vertices in the suffix, which is never sent), the words of its own group
+           block (1/N of the words); plus one small SUM all-reduce of the phase-A partial sums,
+           "still alive" flags and frontier sizes.
   phase C  every rank continues its own groups from level 3 (bit-parallel, as in round-robin).
 
 Result: F[k] = reduced[k] + F_C[k] for the own groups; the global argmin is the usual 8-byte
@@ -27,10 +31,6 @@ import numpy as np
 
 from . import distributed as D
 
-# bytes of pull work per vertex relative to one edge, for the range split (vertices also carry
-# the exchange volume: every vertex's words travel, edges do not)
-DEFAULT_VERTEX_WEIGHT = 8
-
 
 def word_split(K: int, world: int) -> np.ndarray:
     """wbeg[0..world]: rank j owns 64-group words [wbeg[j], wbeg[j+1]) of ceil(K/64)."""
@@ -42,37 +42,58 @@ def own_groups(K: int, wbeg: np.ndarray, rank: int) -> np.ndarray:
     return np.arange(64 * int(wbeg[rank]), min(K, 64 * int(wbeg[rank + 1])), dtype=np.int64)
 
 
-def split_sizes(bounds: np.ndarray, wbeg: np.ndarray, rank: int):
+def part_count(n_eff: int, part: int, nparts: int) -> int:
+    """Number of vertices v = part + i*nparts below n_eff."""
+    return (n_eff - part + nparts - 1) // nparts if n_eff > part else 0
+
+
+def part_vertices(n_eff: int, part: int, nparts: int) -> np.ndarray:
+    return np.arange(part, n_eff, nparts, dtype=np.int64)
+
+
+def split_sizes(n_eff: int, wbeg: np.ndarray, rank: int):
     """(input_split_sizes, output_split_sizes) of the all-to-all, in 64-bit words."""
     world = len(wbeg) - 1
-    cnt = int(bounds[rank + 1] - bounds[rank])
+    cnt = part_count(n_eff, rank, world)
     nw_me = int(wbeg[rank + 1] - wbeg[rank])
     send = [cnt * int(wbeg[j + 1] - wbeg[j]) for j in range(world)]
-    recv = [int(bounds[r + 1] - bounds[r]) * nw_me for r in range(world)]
+    recv = [part_count(n_eff, r, world) * nw_me for r in range(world)]
     return send, recv
 
 
 # ---- numpy emulation of the device layout (tests; documents the kernels' contract) ----------
-def pack_words_np(vis: np.ndarray, lo: int, hi: int, wbeg: np.ndarray) -> np.ndarray:
+def pack_words_np(vis: np.ndarray, part: int, nparts: int, n_eff: int,
+                  wbeg: np.ndarray) -> np.ndarray:
     """Twin of k_pack_words: vis[n, W] (uint64) -> destination-major send buffer."""
     wt = int(wbeg[-1])
-    blk = vis[lo:hi, :wt]
+    blk = vis[part_vertices(n_eff, part, nparts), :wt]
     return np.concatenate([blk[:, wbeg[j]:wbeg[j + 1]].reshape(-1)
                            for j in range(len(wbeg) - 1)]) if wt else np.zeros(0, vis.dtype)
 
 
-def all_to_all_np(sends, bounds: np.ndarray, wbeg: np.ndarray):
+def all_to_all_np(sends, n_eff: int, wbeg: np.ndarray):
     """Emulated all_to_all_single over all ranks: returns every rank's receive buffer."""
     world = len(wbeg) - 1
     outs = []
     for j in range(world):
         parts = []
         for r in range(world):
-            s_sizes, _ = split_sizes(bounds, wbeg, r)
+            s_sizes, _ = split_sizes(n_eff, wbeg, r)
             off = sum(s_sizes[:j])
             parts.append(sends[r][off:off + s_sizes[j]])
         outs.append(np.concatenate(parts) if parts else np.zeros(0, np.uint64))
     return outs
+
+
+def unpack_np(recv: np.ndarray, n: int, n_eff: int, nparts: int, nw: int) -> np.ndarray:
+    """Twin of k_hybrid_setup's indexing: recv -> rows[n, nw] (zero rows beyond n_eff)."""
+    rows = np.zeros((n, nw), dtype=recv.dtype)
+    off = 0
+    for r in range(nparts):
+        vs = part_vertices(n_eff, r, nparts)
+        rows[vs] = recv[off:off + len(vs) * nw].reshape(len(vs), nw)
+        off += len(vs) * nw
+    return rows
 
 
 @dataclass
@@ -85,8 +106,7 @@ class HybridResult:
 class HybridRunner:
     """Reusable buffers + plan for one (solver, K, world) combination."""
 
-    def __init__(self, solver, K: int, ctx: D.DistContext,
-                 vertex_weight: int = DEFAULT_VERTEX_WEIGHT):
+    def __init__(self, solver, K: int, ctx: D.DistContext):
         import torch
 
         self.solver, self.K, self.ctx = solver, int(K), ctx
@@ -94,11 +114,10 @@ class HybridRunner:
         if self.K < 1 or self.K > solver.hybrid_max_groups():
             raise ValueError(f"hybrid mode handles 1..{solver.hybrid_max_groups()} groups per "
                              f"round, got {self.K}")
-        self.bounds = g.hybrid_split(ctx.world, vertex_weight)
+        self.n_eff = g.hybrid_extent()
         self.wbeg = word_split(self.K, ctx.world)
         self.idx = own_groups(self.K, self.wbeg, ctx.rank)
-        self.send_sizes, self.recv_sizes = split_sizes(self.bounds, self.wbeg, ctx.rank)
-        self.lo, self.hi = int(self.bounds[ctx.rank]), int(self.bounds[ctx.rank + 1])
+        self.send_sizes, self.recv_sizes = split_sizes(self.n_eff, self.wbeg, ctx.rank)
         self.nw = int(self.wbeg[ctx.rank + 1] - self.wbeg[ctx.rank])
         dev = torch.device("cuda", g.device)
         self.send = torch.empty(max(1, sum(self.send_sizes)), dtype=torch.int64, device=dev)
@@ -134,29 +153,28 @@ class HybridRunner:
     def run(self, queries) -> HybridResult:
         if queries.K != self.K:
             raise ValueError("query count differs from the plan")
-        out, sa = self.solver.hybrid_phase_a(queries, self.lo, self.hi, self.ctx.rank == 0,
-                                             self.wbeg, self.send.data_ptr())
+        ctx = self.ctx
+        out, sa = self.solver.hybrid_phase_a(queries, ctx.rank, ctx.world, self.n_eff,
+                                             ctx.rank == 0, self.wbeg, self.send.data_ptr())
         reduced = self._exchange(out)
-        Fc, sc = self.solver.hybrid_phase_c(self.K, int(self.wbeg[self.ctx.rank]), self.nw,
-                                            self.recv.data_ptr(), reduced)
+        Fc, sc = self.solver.hybrid_phase_c(self.K, int(self.wbeg[ctx.rank]), self.nw, ctx.world,
+                                            self.n_eff, self.recv.data_ptr(), reduced)
         F = reduced[self.idx] + Fc[:len(self.idx)]
         stats = {"levels": sa.get("levels", 0) + sc.get("levels", 0),
                  "td_levels": sa.get("td_levels", 0) + sc.get("td_levels", 0),
                  "bu_levels": sa.get("bu_levels", 0) + sc.get("bu_levels", 0),
                  "phase_a_ms": sa.get("device_ms"), "phase_c_ms": sc.get("device_ms"),
-                 "range": (self.lo, self.hi), "words": self.nw}
+                 "part": (ctx.rank, ctx.world, self.n_eff), "words": self.nw}
         return HybridResult(self.idx, F, stats)
 
 
-def hybrid_bfs(solver, queries, ctx: Optional[D.DistContext] = None,
-               vertex_weight: int = DEFAULT_VERTEX_WEIGHT) -> HybridResult:
+def hybrid_bfs(solver, queries, ctx: Optional[D.DistContext] = None) -> HybridResult:
     """One-shot hybrid run of all K groups over the ranks of ctx (single process if None)."""
     ctx = ctx or D.DistContext(device=solver.graph.device)
-    return HybridRunner(solver, queries.K, ctx, vertex_weight).run(queries)
+    return HybridRunner(solver, queries.K, ctx).run(queries)
 
 
-def emulate_ranks(solver, queries, world: int, vertex_weight: int = DEFAULT_VERTEX_WEIGHT,
-                  timings: Optional[list] = None) -> np.ndarray:
+def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None) -> np.ndarray:
     """Run the hybrid algorithm for `world` ranks sequentially in ONE process on one GPU (no
     torch.distributed): phase A of every rank, a host-side all-to-all, phase C of every rank.
     Returns the full F vector. Used by the GPU tests and to time per-rank phases: with
@@ -165,31 +183,29 @@ def emulate_ranks(solver, queries, world: int, vertex_weight: int = DEFAULT_VERT
 
     K = queries.K
     g = solver.graph
-    bounds = g.hybrid_split(world, vertex_weight)
+    n_eff = g.hybrid_extent()
     wbeg = word_split(K, world)
     dev = torch.device("cuda", g.device)
     sends, outs = [], []
     for r in range(world):
-        ss, _ = split_sizes(bounds, wbeg, r)
+        ss, rs = split_sizes(n_eff, wbeg, r)
         buf = torch.empty(max(1, sum(ss)), dtype=torch.int64, device=dev)
-        out, sa = solver.hybrid_phase_a(queries, int(bounds[r]), int(bounds[r + 1]), r == 0,
-                                        wbeg, buf.data_ptr())
+        out, sa = solver.hybrid_phase_a(queries, r, world, n_eff, r == 0, wbeg, buf.data_ptr())
         if timings is not None:
-            _, rs = split_sizes(bounds, wbeg, r)
-            timings.append({"rank": r, "range": (int(bounds[r]), int(bounds[r + 1])),
+            timings.append({"rank": r, "vertices": part_count(n_eff, r, world),
                             "phase_a_ms": sa["device_ms"], "send_bytes": 8 * sum(ss),
                             "recv_bytes": 8 * sum(rs), "phase_c_ms": 0.0})
         sends.append(buf[:sum(ss)].cpu().numpy().view(np.uint64))
         outs.append(out)
     reduced = np.sum(outs, axis=0)
-    recvs = all_to_all_np(sends, bounds, wbeg)
+    recvs = all_to_all_np(sends, n_eff, wbeg)
     F = np.zeros(K, dtype=np.int64)
     for j in range(world):
         nw = int(wbeg[j + 1] - wbeg[j])
         if nw == 0:
             continue
         rt = torch.from_numpy(recvs[j].view(np.int64)).to(dev)
-        Fc, sc = solver.hybrid_phase_c(K, int(wbeg[j]), nw, rt.data_ptr(), reduced)
+        Fc, sc = solver.hybrid_phase_c(K, int(wbeg[j]), nw, world, n_eff, rt.data_ptr(), reduced)
         if timings is not None:
             timings[len(timings) - world + j]["phase_c_ms"] = sc["device_ms"]
             timings[len(timings) - world + j]["levels_c"] = sc["levels"]

@@ -32,19 +32,22 @@ def test_word_split_and_exchange_layout(K, world):
     while W < wt:
         W *= 2
     vis = rng.integers(0, 2**63, size=(n, W), dtype=np.uint64)
-    bounds = np.sort(np.concatenate([[0, n], rng.integers(0, n, world - 1)])).astype(np.int64)
-    sends = [H.pack_words_np(vis, int(bounds[r]), int(bounds[r + 1]), wbeg) for r in range(world)]
-    for r in range(world):
-        ss, rs = H.split_sizes(bounds, wbeg, r)
-        assert sum(ss) == len(sends[r])
-    recvs = H.all_to_all_np(sends, bounds, wbeg)
-    for j in range(world):
-        nw = int(wbeg[j + 1] - wbeg[j])
-        _, rs = H.split_sizes(bounds, wbeg, j)
-        assert len(recvs[j]) == sum(rs) == n * nw
-        # rank j holds its words of every vertex, vertex-major (the phase-C input layout)
-        assert np.array_equal(recvs[j].reshape(n, nw) if nw else recvs[j],
-                              vis[:, wbeg[j]:wbeg[j + 1]].reshape(n, nw) if nw else recvs[j])
+    for n_eff in (n, n - 40, 3):  # rows >= n_eff (isolated-vertex suffix) are not exchanged
+        sends = [H.pack_words_np(vis, r, world, n_eff, wbeg) for r in range(world)]
+        assert sum(H.part_count(n_eff, r, world) for r in range(world)) == n_eff
+        for r in range(world):
+            ss, rs = H.split_sizes(n_eff, wbeg, r)
+            assert sum(ss) == len(sends[r])
+        recvs = H.all_to_all_np(sends, n_eff, wbeg)
+        for j in range(world):
+            nw = int(wbeg[j + 1] - wbeg[j])
+            _, rs = H.split_sizes(n_eff, wbeg, j)
+            assert len(recvs[j]) == sum(rs) == n_eff * nw
+            # rank j holds its words of every vertex (the phase-C input, k_hybrid_setup order)
+            rows = H.unpack_np(recvs[j], n, n_eff, world, nw)
+            want = vis[:, wbeg[j]:wbeg[j + 1]].copy()
+            want[n_eff:] = 0
+            assert np.array_equal(rows, want)
 
 
 def _free_port():
@@ -63,14 +66,12 @@ def _a2a_worker(rank, world, port, out_dir):
     from msbfs.parallel import distributed as D
     from msbfs.parallel import hybrid as H
     ctx = D.init_from_env(backend="gloo", use_gpu=False)
-    K, n = 700, 101
+    K, n, n_eff = 700, 101, 90
     wbeg = H.word_split(K, world)
-    bounds = np.array([0, 7, 60, n][:world] + [n], dtype=np.int64) if world > 1 else \
-        np.array([0, n], dtype=np.int64)
     rng = np.random.default_rng(5)
     vis = rng.integers(0, 2**62, size=(n, 16), dtype=np.uint64)
-    send = H.pack_words_np(vis, int(bounds[rank]), int(bounds[rank + 1]), wbeg)
-    ss, rs = H.split_sizes(bounds, wbeg, rank)
+    send = H.pack_words_np(vis, rank, world, n_eff, wbeg)
+    ss, rs = H.split_sizes(n_eff, wbeg, rank)
     r = torch.empty(sum(rs), dtype=torch.int64)
     dist.all_to_all_single(r, torch.from_numpy(send.view(np.int64)), rs, ss)
     np.save(os.path.join(out_dir, f"a2a{rank}.npy"), r.numpy())
@@ -81,14 +82,16 @@ def _a2a_worker(rank, world, port, out_dir):
 def test_gloo_all_to_all_matches_emulation(tmp_path, world):
     H = _H()
     mp.spawn(_a2a_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    K, n = 700, 101
+    K, n, n_eff = 700, 101, 90
     wbeg = H.word_split(K, world)
     rng = np.random.default_rng(5)
     vis = rng.integers(0, 2**62, size=(n, 16), dtype=np.uint64)
     for j in range(world):
+        nw = int(wbeg[j + 1] - wbeg[j])
         got = np.load(tmp_path / f"a2a{j}.npy").view(np.uint64)
-        want = vis[:, wbeg[j]:wbeg[j + 1]].reshape(-1)
-        assert np.array_equal(got, want)
+        want = vis[:, wbeg[j]:wbeg[j + 1]].copy()
+        want[n_eff:] = 0
+        assert np.array_equal(H.unpack_np(got, n, n_eff, world, nw), want)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-rank cost of the hybrid decomposition on ONE GPU (no multi-GPU box needed).
 
-Runs every rank's phase A (levels 1-2, own vertex range) and phase C (own groups, levels >= 3)
+Runs every rank's phase A (levels 1-2, own residue class of vertices) and phase C (own groups, levels >= 3)
 sequentially on one GPU (parallel/hybrid.py emulate_ranks), checks F against the single-GPU
 solver, and prints per-rank device times plus the all-to-all volume. The estimated N-GPU step
 is max_r(A_r) + exchange + max_r(C_r); the exchange is priced at --a2a-gbps per GPU (receive
@@ -28,10 +28,9 @@ def main():
     ap.add_argument("--groups", type=int, default=1024)
     ap.add_argument("--group-size", type=int, default=16)
     ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
-    ap.add_argument("--vertex-weight", type=int, default=8)
     ap.add_argument("--no-roundrobin", action="store_true")
     ap.add_argument("--a2a-gbps", type=float, default=300.0,
-                    help="assumed per-GPU all-to-all receive bandwidth (GB/s)")
+                    help="assumed per-GPU all-to-all bandwidth (GB/s, max of send and receive)")
     args = ap.parse_args()
 
     import msbfs
@@ -48,13 +47,13 @@ def main():
         print(json.dumps({"ranks": 1, "ms": round(one, 3), "device_ms": ref.stats["device_ms"]}),
               flush=True)
         for N in args.ranks:
-            H.emulate_ranks(s, qs, N, args.vertex_weight)  # warm
+            H.emulate_ranks(s, qs, N)  # warm
             tim = []
-            F = H.emulate_ranks(s, qs, N, args.vertex_weight, timings=tim)
+            F = H.emulate_ranks(s, qs, N, timings=tim)
             ok = bool(np.array_equal(F, ref.F))
             a = max(x["phase_a_ms"] for x in tim)
             c = max(x["phase_c_ms"] for x in tim)
-            rb = max(x["recv_bytes"] for x in tim)
+            rb = max(max(x["recv_bytes"], x["send_bytes"]) for x in tim)
             x_ms = rb / (args.a2a_gbps * 1e9) * 1e3
             rr = [0.0]
             for r in ([] if args.no_roundrobin else range(N)):
@@ -62,7 +61,7 @@ def main():
                 rr.append(s.run(sub).stats["device_ms"])
             print(json.dumps({
                 "ranks": N, "correct": ok, "phase_a_ms_max": round(a, 3),
-                "phase_c_ms_max": round(c, 3), "a2a_recv_MB_max": round(rb / 2**20, 1),
+                "phase_c_ms_max": round(c, 3), "a2a_MB_max": round(rb / 2**20, 1),
                 "a2a_ms_est": round(x_ms, 3), "hybrid_est_ms": round(a + x_ms + c, 3),
                 "roundrobin_ms_max": round(max(rr), 3),
                 "per_rank": [{k: (round(v, 3) if isinstance(v, float) else v)
