@@ -497,19 +497,30 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// bottom-up, narrow vertices: G lanes per vertex, U neighbours in flight per lane, early exit
-// when every alive group is covered.
+// bottom-up, narrow vertices: G lanes per vertex, early exit when every alive group is covered.
+// Each step takes C = 8 neighbours: the group's G lanes load and filter them cooperatively
+// (8/G column ids + 8/G bitmap probes per lane instead of 8 + 8), then every lane pulls its
+// slot of each surviving neighbour's row (ids broadcast inside the group by shuffles).
+// BT = block size; HUBW > 0: probes of the HUBW*32 lowest ids (hubs) read an LDS snapshot of
+// the visited bitmap (see k_bu_chunks; big blocks amortise the copy).
 // ---------------------------------------------------------------------------------------------
-template <int W, bool COUNT, int U>
-__global__ __launch_bounds__(kBlock) void k_bu_narrow(
+template <int W, bool COUNT, int BT, int HUBW>
+__global__ __launch_bounds__(BT) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
     int next_wide) {
   using L = Lay<W>;
-  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
+  constexpr int NWV = BT / 64, TILE = NWV * VPW;
+  constexpr int C = 8;                       // neighbours per step
+  constexpr int Q = C / G > 0 ? C / G : 1;   // ids loaded per lane per step
+  static_assert(G * Q == C, "lane groups of 1..8 lanes");
   __shared__ LdsQueue qa, qf, qw;
-  __shared__ unsigned long long scratch[kWaves];
+  __shared__ unsigned long long scratch[NWV];
+  __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
+  if constexpr (HUBW > 0)
+    for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
   q_init(qa);
   q_init(qf);
   q_init(qw);
@@ -541,28 +552,37 @@ __global__ __launch_bounds__(kBlock) void k_bu_narrow(
     }
     const bool g_open = valid && ((__ballot(lane_open) >> (sub * G)) & L::GBITS);
     if (g_open) {
-      int64_t e = beg;
-      while (e < end) {
-        int32_t u[U];
+      for (int64_t e = beg; e < end; e += C) {
+        int32_t u[Q];
 #pragma unroll
-        for (int q = 0; q < U; ++q) u[q] = (e + q < end) ? col[e + q] : -1;
-        // ids below filter_from (degree-ordered hubs: rows hot in cache) are loaded directly;
-        // the long tail is first tested against the visited bitmap (one request either way)
+        for (int q = 0; q < Q; ++q) {
+          const int64_t ee = e + q * G + slot;
+          u[q] = ee < end ? col[ee] : -1;
+        }
+        // ids below filter_from are loaded without a probe (filter off: filter_from = INT_MAX)
 #pragma unroll
-        for (int q = 0; q < U; ++q)
-          if (u[q] >= filter_from && !any_visited(anyvis, u[q])) u[q] = -1;
-        V<VW> x[U];
+        for (int q = 0; q < Q; ++q) {
+          if (u[q] >= filter_from) {
+            bool vis;
+            if (HUBW > 0 && u[q] < HUBW * 32) vis = (hub[u[q] >> 5] >> (u[q] & 31)) & 1u;
+            else vis = any_visited(anyvis, u[q]);
+            if (!vis) u[q] = -1;
+          }
+        }
+        V<VW> x[C];
 #pragma unroll
-        for (int q = 0; q < U; ++q)
-          x[q] = u[q] >= 0 ? ldv<VW>(R + (int64_t)u[q] * W + slot * VW) : vzero<VW>();
+        for (int c = 0; c < C; ++c) {
+          // candidate c = column entry e + c: lane (c % G) of this group holds it in u[c / G]
+          const int32_t uc = G == 1 ? u[c] : __shfl(u[c / G], sub * G + (c % G));
+          x[c] = uc >= 0 ? ldv<VW>(R + (int64_t)uc * W + slot * VW) : vzero<VW>();
+        }
         bool cov = true;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
 #pragma unroll
-          for (int q = 0; q < U; ++q) acc.w[j] |= x[q].w[j];
+          for (int c = 0; c < C; ++c) acc.w[j] |= x[c].w[j];
           cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
         }
-        e += U;
         // the whole group runs this loop in lock step (same v); exit when all lanes covered
         if (!((__ballot(!cov) >> (sub * G)) & L::GBITS)) break;
       }
@@ -1055,7 +1075,6 @@ class BitparSolver final : public Solver {
     hctr_ = std::make_unique<PinnedBuf>(sizeof(Ctr));
     hsmall_ = std::make_unique<PinnedBuf>(small_.bytes);
     if (const char* d = getenv("MSBFS_DIRS")) dirs_ = d;  // per-level T/B override (tuning)
-    if (const char* u = getenv("MSBFS_UNROLL")) unroll_ = atoi(u);
     if (const char* w = getenv("MSBFS_WIDE_LATER")) wide_later_ = atoi(w);
     if (const char* x = getenv("MSBFS_X")) xmode_ = atoi(x);          // experiments only
     if (const char* t = getenv("MSBFS_TILE")) tile_ = atoi(t);
@@ -1244,11 +1263,10 @@ class BitparSolver final : public Solver {
   std::unique_ptr<PinnedBuf> hctr_, hsmall_;
   int32_t epoch_ = 0;
   std::string dirs_;
-  int unroll_ = 8;
   int wide_later_ = 1024;
   int xmode_ = 0;
   int tile_ = 256;
-  int hub_lds_ = 1;
+  int hub_lds_ = 3;  // bit 0: chunks kernel, bit 1: narrow kernel (MSBFS_HUBLDS)
   int64_t n_eff_ = 0;
   const void* eff_key_[3] = {nullptr, nullptr, nullptr};
 };
@@ -1409,14 +1427,25 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       const int64_t hub_ids = g_.old2new ? (int64_t)(hub_bytes_ / (8.0 * W)) : 0;
       const int32_t filter_from =
           filter ? (int32_t)std::min<int64_t>(hub_ids, INT32_MAX) : INT32_MAX;
+      constexpr int kHubW = 14336;  // 56 KB of LDS: ids < 458752
+      const bool hub_lds = hub_lds_ && filter_from == 0 && n > (int64_t)kHubW * 32 * 4;
       if (S.nact) {
-        auto kern = unroll_ >= 8 ? k_bu_narrow<W, COUNT, 8> : k_bu_narrow<W, COUNT, 4>;
-        const int gn = grid_for(S.nact, L::TILE, grid);
-        kern<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
-                                   sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
-                                   fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
-                                   anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                                   next_wide);
+        if (hub_lds && (hub_lds_ & 2)) {
+          constexpr int BT = 1024;
+          const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
+          k_bu_narrow<W, COUNT, BT, kHubW><<<gn, BT, 0, s>>>(
+              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+              done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+              next_wide);
+        } else {
+          const int gn = grid_for(S.nact, L::TILE, grid);
+          k_bu_narrow<W, COUNT, kBlock, 0><<<gn, kBlock, 0, s>>>(
+              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+              done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+              next_wide);
+        }
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       if (S.nactw) {
@@ -1427,9 +1456,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         k_chunk_owner<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(offs_.as<int64_t>(), S.nactw,
                                                                    owner_.as<int32_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
-        constexpr int kHubW = 14336;  // 56 KB of LDS: ids < 458752
-        const bool hub_lds = hub_lds_ && filter_from == 0 && n > (int64_t)kHubW * 32 * 4;
-        if (hub_lds) {
+        if (hub_lds && (hub_lds_ & 1)) {
           k_bu_chunks<W, 256, 1024, kHubW><<<grid_for(chunks_max, 16, 512), 1024, 0, s>>>(
               actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
               sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
