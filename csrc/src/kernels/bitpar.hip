@@ -190,6 +190,9 @@ struct BitCounter {
   }
   template <int W, bool COUNT>
   __device__ __forceinline__ void spill(Lds<W, COUNT>& s, int slot) {
+    spill(s.f, slot);
+  }
+  __device__ __forceinline__ void spill(uint32_t* f, int slot) {
 #pragma unroll
     for (int j = 0; j < VW; ++j) {
       uint64_t any = 0;
@@ -202,7 +205,7 @@ struct BitCounter {
         uint32_t v = 0;
 #pragma unroll
         for (int d = 0; d < D; ++d) v |= (uint32_t)((c[j][d] >> b) & 1ull) << d;
-        atomicAdd(&s.f[base + b], v);
+        atomicAdd(&f[base + b], v);
       }
 #pragma unroll
       for (int d = 0; d < D; ++d) c[j][d] = 0;
@@ -504,12 +507,17 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
 // BT = block size; HUBW > 0: probes of the HUBW*32 lowest ids (hubs) read an LDS snapshot of
 // the visited bitmap (see k_bu_chunks; big blocks amortise the copy).
 // ---------------------------------------------------------------------------------------------
-template <int W, bool COUNT, int BT, int HUBW>
+//
+// FUSE: the level's new-bit counts are accumulated here (register bit-sliced counters -> LDS ->
+// this block's row of the counter slab, slabF = first row of this launch) instead of by a
+// separate k_count_frontier pass that re-reads both rows of every new frontier vertex.
+template <int W, bool COUNT, int BT, int HUBW, bool FUSE>
 __global__ __launch_bounds__(BT) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
-    int next_wide) {
+    int next_wide, uint32_t* slabF) {
+  static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
   constexpr int NWV = BT / 64, TILE = NWV * VPW;
@@ -519,8 +527,11 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
   __shared__ LdsQueue qa, qf, qw;
   __shared__ unsigned long long scratch[NWV];
   __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
+  __shared__ uint32_t cnt[FUSE ? 64 * W : 1];
   if constexpr (HUBW > 0)
     for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
+  if constexpr (FUSE)
+    for (int i = threadIdx.x; i < 64 * W; i += BT) cnt[i] = 0;
   q_init(qa);
   q_init(qf);
   q_init(qw);
@@ -531,6 +542,9 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long eu = 0, ef = 0, ev = 0;
+  BitCounter<VW> bc;
+  int nadd = 0;
+  if constexpr (FUSE) bc.zero();
   for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nact; tb += (int64_t)gridDim.x * TILE) {
     const int64_t idx = tb + wv * VPW + sub;
     const bool valid = idx < nact;
@@ -601,6 +615,13 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
       for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
       stv<VW>(Wb + (int64_t)v * W + slot * VW, nv);
     }
+    if constexpr (FUSE) {  // nw is zero for invalid lanes
+      bc.add(nw);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.spill(cnt, slot);
+        nadd = 0;
+      }
+    }
     const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
     const bool g_new = (bn >> (sub * G)) & L::GBITS;
     const bool g_nf = (bf >> (sub * G)) & L::GBITS;
@@ -630,6 +651,12 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
+  if constexpr (FUSE) {
+    bc.spill(cnt, slot);
+    __syncthreads();
+    uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+    for (int i = threadIdx.x; i < 64 * W; i += BT) row[i] = cnt[i];
+  }
 }
 
 // bottom-up, wide vertices, phase 1: one wave per edge chunk (<= kChunk edges), processed in
@@ -805,19 +832,25 @@ __global__ __launch_bounds__(kBlock) void k_chunk_owner(const int64_t* offs, int
 }
 
 // bottom-up, wide vertices, phase 2: G lanes per vertex fold acc[v] into the visited words.
-template <int W, bool COUNT>
+template <int W, bool COUNT, bool FUSE>
 __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, uint64_t* Wb,
     uint64_t* acc, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* actw2,
-    int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* act2n, int next_wide) {
+    int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* act2n, int next_wide, uint32_t* slabF) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ LdsQueue qa, qf, qn;
   __shared__ unsigned long long scratch[kWaves];
+  __shared__ uint32_t cnt[FUSE ? 64 * W : 1];
+  if constexpr (FUSE)
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock) cnt[i] = 0;
   q_init(qa);
   q_init(qf);
   q_init(qn);
   __syncthreads();
+  BitCounter<VW> bc;
+  int nadd = 0;
+  if constexpr (FUSE) bc.zero();
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
   const int wv = threadIdx.x >> 6;
   V<VW> am;
@@ -850,6 +883,13 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
       stv<VW>(Wb + vo, nv);
       deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
     }
+    if constexpr (FUSE) {  // nwb is zero for invalid lanes
+      bc.add(nwb);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.spill(cnt, slot);
+        nadd = 0;
+      }
+    }
     const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
     const bool g_new = (bn >> (sub * G)) & L::GBITS;
     const bool g_nf = (bf >> (sub * G)) & L::GBITS;
@@ -878,6 +918,12 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
+  if constexpr (FUSE) {
+    bc.spill(cnt, slot);
+    __syncthreads();
+    uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1079,6 +1125,7 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_X")) xmode_ = atoi(x);          // experiments only
     if (const char* t = getenv("MSBFS_TILE")) tile_ = atoi(t);
     if (const char* h = getenv("MSBFS_HUBLDS")) hub_lds_ = atoi(h);
+    if (const char* f = getenv("MSBFS_FUSE_COUNT")) fuse_count_ = atoi(f);
     MSBFS_HIP_CHECK(hipDeviceSynchronize());
   }
 
@@ -1267,6 +1314,7 @@ class BitparSolver final : public Solver {
   int xmode_ = 0;
   int tile_ = 256;
   int hub_lds_ = 3;  // bit 0: chunks kernel, bit 1: narrow kernel (MSBFS_HUBLDS)
+  int fuse_count_ = 1;  // MSBFS_FUSE_COUNT=0: separate k_count_frontier pass
   int64_t n_eff_ = 0;
   const void* eff_key_[3] = {nullptr, nullptr, nullptr};
 };
@@ -1429,22 +1477,31 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           filter ? (int32_t)std::min<int64_t>(hub_ids, INT32_MAX) : INT32_MAX;
       constexpr int kHubW = 14336;  // 56 KB of LDS: ids < 458752
       const bool hub_lds = hub_lds_ && filter_from == 0 && n > (int64_t)kHubW * 32 * 4;
+      // counting fused into the traversal kernels (the edge-count pass keeps k_count_frontier)
+      constexpr bool FUSE = !COUNT;
+      const bool fuse = FUSE && fuse_count_;
       if (S.nact) {
         if (hub_lds && (hub_lds_ & 2)) {
           constexpr int BT = 1024;
           const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
-          k_bu_narrow<W, COUNT, BT, kHubW><<<gn, BT, 0, s>>>(
-              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
-              done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-              next_wide);
+          auto kn = fuse ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE>
+                         : k_bu_narrow<W, COUNT, BT, kHubW, false>;
+          kn<<<gn, BT, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
+                               sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
+                               fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+                               anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+                               next_wide, slabF(rows));
+          if (fuse) rows += gn;
         } else {
           const int gn = grid_for(S.nact, L::TILE, grid);
-          k_bu_narrow<W, COUNT, kBlock, 0><<<gn, kBlock, 0, s>>>(
-              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
-              done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-              next_wide);
+          auto kn = fuse ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE>
+                         : k_bu_narrow<W, COUNT, kBlock, 0, false>;
+          kn<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
+                                   sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
+                                   fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+                                   anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+                                   next_wide, slabF(rows));
+          if (fuse) rows += gn;
         }
         MSBFS_HIP_CHECK(hipGetLastError());
       }
@@ -1471,13 +1528,16 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         }
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(S.nactw, L::TILE, grid);
-        k_bu_wide_finalize<W, COUNT><<<gw, kBlock, 0, s>>>(
+        auto kf = fuse ? k_bu_wide_finalize<W, COUNT, FUSE> : k_bu_wide_finalize<W, COUNT, false>;
+        kf<<<gw, kBlock, 0, s>>>(
             actw_[0].as<int32_t>(), S.nactw, g_.rowptr, R, O, acc_[S.ac].as<uint64_t>(), alive,
             sm.gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), act_[1].as<int32_t>(), next_wide);
+            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), act_[1].as<int32_t>(), next_wide,
+            slabF(rows));
         MSBFS_HIP_CHECK(hipGetLastError());
+        if (fuse) rows += gw;
       }
-      {
+      if (!fuse) {
         // new frontier bits = Wb & ~R (both still in place: the swap is below)
         const int gc = grid_for(S.nact + S.nactw, L::TILE, grid);
         k_count_frontier<W, COUNT, true><<<gc, kBlock, 0, s>>>(
