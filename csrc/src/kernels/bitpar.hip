@@ -1063,11 +1063,19 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
   }
 }
 
-// n_eff = 1 + the last vertex with deg > 0 (0 if none)
+// n_eff = 1 + the last vertex with deg > 0 (0 if none): per-thread max, wave max, one atomic
+// per wave (atomics on one address serialise)
 __global__ void k_extent(const int64_t* rowptr, int64_t n, unsigned long long* out) {
+  unsigned long long m = 0;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
        v += (int64_t)gridDim.x * blockDim.x)
-    if (rowptr[v + 1] > rowptr[v]) atomicMax(out, (unsigned long long)(v + 1));
+    if (rowptr[v + 1] > rowptr[v]) m = (unsigned long long)(v + 1);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(m, off);
+    m = o > m ? o : m;
+  }
+  if (lane_id() == 0 && m) atomicMax(out, m);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1709,7 +1717,7 @@ int64_t hybrid_extent(const DeviceGraph& g) {
   DevBuf d;
   d.alloc(sizeof(unsigned long long));
   MSBFS_HIP_CHECK(hipMemset(d.p, 0, sizeof(unsigned long long)));
-  bp::k_extent<<<grid_for(g.n, 256, 8192), 256>>>(g.rowptr, g.n, d.as<unsigned long long>());
+  bp::k_extent<<<grid_for(g.n, 256, 2048), 256>>>(g.rowptr, g.n, d.as<unsigned long long>());
   MSBFS_HIP_CHECK(hipGetLastError());
   unsigned long long h = 0;
   MSBFS_HIP_CHECK(hipMemcpy(&h, d.p, sizeof(h), hipMemcpyDeviceToHost));

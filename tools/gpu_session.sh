@@ -72,6 +72,9 @@ for s in "$@"; do
            step road_1024 600 python tools/bench_graph.py --graph grid:2048:2048:0.7 --groups 1024 --force-dir 1
            step rmat_a4 600 python tools/bench_graph.py --graph rmat:24:16 --groups 1024 --alpha 4 --relabel 1
            step rmat_a14 600 python tools/bench_graph.py --graph rmat:24:16 --groups 1024 --relabel 1 ;;
+    rmat22) step rmat22 300 python bench.py --scale 22 --groups 64 --steps 5 --warmup 1 --verify 16 ;;
+    usaroad) step usaroad 900 python tools/bench_graph.py --graph grid:4896:4896:0.6 --groups 64 --steps 1 ;;
+    hybsimall) step hybsimall 900 python tools/hybrid_sim.py --scale 26 --ranks 2 4 8 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
