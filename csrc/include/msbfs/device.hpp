@@ -78,6 +78,9 @@ struct DeviceGraph {
   // (null when the graph keeps the user's ids). Solvers map query sources through it.
   int32_t* old2new = nullptr;
   DevBuf own_old2new;
+  // every row's neighbour ids ascending (device_graph_sort_rows; relabelling sorts too). Solvers
+  // may binary-search rows only when this is set.
+  bool rows_sorted = false;
 };
 
 // Stats returned by solvers (mirrors msbfs_stats in msbfs.h).
@@ -160,6 +163,10 @@ std::unique_ptr<Solver> make_sweep_solver(const DeviceGraph& g);
 // Inclusive prefix sum of ceil(degree / chunk) over `list[0..cnt)` into offs[0..cnt) (int64);
 // chunk = 1 gives the frontier's edge prefix used by the load-balanced top-down expansions.
 size_t frontier_scan_temp_bytes(int64_t max_items);
+// plain inclusive prefix sum of int64 values (hipcub); temp >= inclusive_scan_temp_bytes(cnt)
+size_t inclusive_scan_temp_bytes(int64_t max_items);
+void inclusive_scan_i64(const int64_t* in, int64_t* out, int64_t cnt, void* temp,
+                        size_t temp_bytes, hipStream_t s);
 void frontier_degree_scan(const int64_t* rowptr, const int32_t* list, int64_t cnt, int64_t* offs,
                           void* temp, size_t temp_bytes, hipStream_t s, int64_t chunk = 1);
 

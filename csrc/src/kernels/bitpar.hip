@@ -93,6 +93,17 @@ __device__ __forceinline__ V<VW> vzero() {
   return r;
 }
 
+// Wave-uniform copies (SGPRs) of values every lane holds identically: keeps loops over them
+// uniform (scalar branches) instead of exec-masked "divergent" loops.
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int32_t uni32(int32_t x) {
+  return (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
 struct Ctr {
   Slot32 act2, actw2, fl2, touched;
   Slot64 ef2;  // sum of degrees of the next frontier
@@ -676,24 +687,142 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
 // bit another kernel of this level sets later belongs to a vertex first visited at this level,
 // whose row in R is still zero, so skipping it is exact. Big blocks (BT threads, 2 per CU)
 // amortise the copy; the grid is persistent (grid-stride over chunks).
+// One wave pulls edges [beg, lim) of wide vertex v (a chunk) and publishes the new bits into
+// acc[v] (k_bu_wide_finalize folds them in). coop: chunks of one vertex run concurrently and
+// share progress through acc (see below); coop = 0 (first bottom-up level) skips that.
+template <int W, int T, int HUBW>
+__device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, const int32_t* col,
+                                           const uint64_t* R, const V<Lay<W>::VW>& am,
+                                           uint64_t* acc, const uint32_t* anyvis,
+                                           const uint32_t* hub, int32_t filter_from, int coop,
+                                           int xmode, int32_t* lst) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, S = L::VPW;
+  constexpr int PB = 8;  // rows in flight per lane group in phase B
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int64_t vo = (int64_t)v * W + slot * VW;
+  const V<VW> r = ldv<VW>(R + vo);
+  // g = bits the vertex's other chunks have published so far. Chunks of one hub run
+  // concurrently, so each tile publishes its partial OR with a RETURNING atomicOr that also
+  // hands back the current union from the memory side (atomics bypass the non-coherent per-XCD
+  // L2s); every chunk stops once the union covers all alive groups.
+  V<VW> g = vzero<VW>();
+  if (coop) {
+    if (sub == 0) {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) g.w[j] = atomicOr((unsigned long long*)&acc[vo + j], 0ull);
+    }
+#pragma unroll
+    for (int j = 0; j < VW; ++j) g.w[j] = __shfl(g.w[j], slot);  // lane slot of sub-group 0
+  }
+  V<VW> unv, a = vzero<VW>();
+  bool lane_open = false;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    unv.w[j] = ~r.w[j] & am.w[j];
+    lane_open |= (unv.w[j] & ~g.w[j]) != 0;
+  }
+  if (!__ballot(lane_open)) return;  // wave-uniform
+  bool covered = false;
+  for (int64_t t0 = beg; t0 < lim && !covered; t0 += T) {
+    // ---- phase A: ids of this tile, filtered, compacted into lst[0..cnt)
+    constexpr int Q = T / 64;
+    int32_t u[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int64_t e = t0 + q * 64 + lane;
+      u[q] = e < lim ? col[e] : -1;
+    }
+    if (!(xmode & 2)) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        bool vis;
+        if (HUBW > 0 && u[q] >= 0 && u[q] < HUBW * 32)
+          vis = (hub[u[q] >> 5] >> (u[q] & 31)) & 1u;
+        else
+          vis = u[q] < filter_from || any_visited(anyvis, u[q]);
+        if (u[q] >= 0 && !vis) u[q] = -1;
+      }
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint64_t m = __ballot(u[q] >= 0);
+      if (u[q] >= 0) lst[cnt + __popcll(m & lanemask_lt())] = u[q];
+      cnt += __popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- phase B: rows of the surviving neighbours, PB per lane group per step
+    for (int b = 0; b < cnt; b += PB * S) {
+      int32_t uu[PB];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int k = b + q * S + sub;
+        uu[q] = k < cnt ? lst[k] : -1;
+      }
+#pragma unroll
+      for (int q = 0; q < PB; ++q)
+        if (uu[q] >= 0 && !(xmode & 1)) {
+          const V<VW> x = ldv<VW>(R + (int64_t)uu[q] * W + slot * VW);
+#pragma unroll
+          for (int j = 0; j < VW; ++j) a.w[j] |= x.w[j];
+        }
+#pragma unroll
+      for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+        for (int j = 0; j < VW; ++j) a.w[j] |= __shfl_xor(a.w[j], off);
+      bool cov = true;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
+      if (!__ballot(!cov)) {
+        covered = true;
+        break;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // lst is rewritten by the next tile
+    // publish this chunk's bits so far and pick up the other chunks' (one round trip)
+    if (coop && !covered && t0 + T < lim) {
+      bool cov = true;
+      if (sub == 0) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          const uint64_t nb = a.w[j] & unv.w[j] & ~g.w[j];
+          g.w[j] |= nb ? atomicOr((unsigned long long*)&acc[vo + j], nb)
+                       : atomicOr((unsigned long long*)&acc[vo + j], 0ull);
+          g.w[j] |= nb;
+          cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
+        }
+      }
+      if (!__ballot(!cov)) covered = true;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) g.w[j] = __shfl(g.w[j], slot);
+    }
+  }
+  if (sub == 0) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const uint64_t nb = a.w[j] & unv.w[j] & ~g.w[j];
+      if (nb) atomicOr((unsigned long long*)&acc[vo + j], nb);
+    }
+  }
+}
+
 template <int W, int T, int BT, int HUBW>
 __global__ __launch_bounds__(BT) void k_bu_chunks(
     const int32_t* wl, int64_t nw, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, const uint64_t* alive, const uint64_t* gmask, uint64_t* acc,
     const uint32_t* anyvis, int32_t filter_from, int coop, int xmode, const int32_t* owner) {
   using L = Lay<W>;
-  constexpr int VW = L::VW, G = L::G, S = L::VPW;
-  // T = edges per tile
-  constexpr int PB = 8;   // rows in flight per lane group in phase B
+  constexpr int VW = L::VW, G = L::G;
   __shared__ int32_t tile[BT / 64][T];
   __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
   if constexpr (HUBW > 0) {
     for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
     __syncthreads();
   }
-  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int slot = lane_id() % G;
   int32_t* lst = tile[threadIdx.x >> 6];
-  const int64_t nchunks = offs[nw - 1];
+  const int64_t nchunks = uni64(offs[nw - 1]);
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   V<VW> am;
@@ -705,117 +834,146 @@ __global__ __launch_bounds__(BT) void k_bu_chunks(
   // come after its earlier ones have published their bits and are skipped at the first check.
   // owner[c] = index of chunk c's vertex in wl: one load instead of a ~20-step dependent binary
   // search over offs.
-  const int64_t cstart = coop ? nchunks * wave / nwaves : wave;
-  const int64_t cend = coop ? nchunks * (wave + 1) / nwaves : nchunks;
-  const int64_t cstep = coop ? 1 : nwaves;
+  const int64_t cstart = uni64(coop ? nchunks * wave / nwaves : wave);
+  const int64_t cend = uni64(coop ? nchunks * (wave + 1) / nwaves : nchunks);
+  const int64_t cstep = uni64(coop ? 1 : nwaves);
   for (int64_t c = cstart; c < cend; c += cstep) {
-    const int64_t i = owner[c];
+    const int64_t i = uni32(owner[c]);
+    const int32_t v = uni32(wl[i]);
+    const int64_t j0 = c - (i ? uni64(offs[i - 1]) : 0);
+    const int64_t beg = uni64(rowptr[v]) + j0 * kChunk;
+    const int64_t lim = min(uni64(rowptr[v + 1]), beg + (int64_t)kChunk);
+    chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop, xmode,
+                           lst);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// XCD-labelled chunks (first bottom-up level). There every unvisited vertex scans its whole row
+// and gathers the 8*W-byte visited row of every level-1-frontier neighbour; those rows (tens of
+// MB at W = 16) do not fit one XCD's 4 MB L2, so most gathers went to the Infinity Cache. Here
+// the neighbour-id space is cut into kLabels ranges and each wide vertex's (sorted) row into
+// the matching segments; segment chunks of range x go to blocks with blockIdx % 8 == x, which
+// share an XCD under the observed round-robin dispatch, so each XCD's L2 holds only its range's
+// rows. Placement is a speed hint only: any block may run any chunk (waves steal from the other
+// ranges' queues once their own is empty), so correctness never depends on it.
+// seg[x*nw + i] = first column position of range x in wide vertex i's row (x = 0..kLabels).
+// ---------------------------------------------------------------------------------------------
+constexpr int kLabels = 8;
+struct LabelBounds {
+  int32_t b[kLabels + 1];  // neighbour id ranges [b[x], b[x+1])
+};
+
+__global__ __launch_bounds__(kBlock) void k_seg_split(const int32_t* wl, int64_t nw,
+                                                      const int64_t* rowptr, const int32_t* col,
+                                                      LabelBounds lb, int64_t* seg) {
+  const int64_t total = nw * (kLabels + 1);
+  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = t % nw;
+    const int x = (int)(t / nw);
     const int32_t v = wl[i];
-    const int64_t j0 = c - (i ? offs[i - 1] : 0);
-    const int64_t end = rowptr[v + 1];
-    const int64_t beg = rowptr[v] + j0 * kChunk;
-    const int64_t lim = min(end, beg + (int64_t)kChunk);
-    const int64_t vo = (int64_t)v * W + slot * VW;
-    const V<VW> r = ldv<VW>(R + vo);
-    // g = bits the vertex's other chunks have published so far. Chunks of one hub run
-    // concurrently, so each tile publishes its partial OR with a RETURNING atomicOr that also
-    // hands back the current union from the memory side (atomics bypass the non-coherent per-XCD
-    // L2s); every chunk stops once the union covers all alive groups.
-    V<VW> g = vzero<VW>();
-    if (sub == 0) {
-#pragma unroll
-      for (int j = 0; j < VW; ++j) g.w[j] = atomicOr((unsigned long long*)&acc[vo + j], 0ull);
+    int64_t lo = rowptr[v], hi = rowptr[v + 1];
+    if (x == 0) {
+      seg[i] = lo;
+    } else if (x == kLabels) {
+      seg[(int64_t)kLabels * nw + i] = hi;
+    } else {
+      const int32_t key = lb.b[x];
+      while (lo < hi) {  // first position with col >= key (rows are sorted)
+        const int64_t mid = (lo + hi) >> 1;
+        if (col[mid] < key) lo = mid + 1;
+        else hi = mid;
+      }
+      seg[(int64_t)x * nw + i] = lo;
     }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_seg_counts(const int64_t* seg, int64_t nw,
+                                                       int64_t* cnt) {
+  const int64_t total = nw * kLabels;
+  for (int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x; f < total;
+       f += (int64_t)gridDim.x * kBlock) {
+    const int64_t len = max(seg[f + nw] - seg[f], (int64_t)0);  // (sorted rows: never < 0)
+    cnt[f] = (len + kChunk - 1) / kChunk;
+  }
+}
+
+// owner[c] = f (= x*nw + i) for every chunk c of segment f (P = inclusive chunk-count prefix)
+__global__ __launch_bounds__(kBlock) void k_seg_owner(const int64_t* P, int64_t nf,
+                                                      int32_t* owner) {
+  for (int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x; f < nf;
+       f += (int64_t)gridDim.x * kBlock) {
+    const int64_t e = P[f];
+    for (int64_t c = f ? P[f - 1] : 0; c < e; ++c) owner[c] = (int32_t)f;
+  }
+}
+
+// b[x] = first vertex v with rowptr[v] >= x/kLabels of the edge endpoints (equal endpoint mass
+// per range: after degree relabelling range 0 is a few hundred hubs, the last one the tail)
+__global__ void k_label_bounds(const int64_t* rowptr, int64_t n, int32_t* b) {
+  const int x = (int)threadIdx.x;
+  if (x > kLabels) return;
+  const int64_t total = rowptr[n];
+  const int64_t target = total / kLabels * x + total % kLabels * x / kLabels;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rowptr[mid] >= target) hi = mid;
+    else lo = mid + 1;
+  }
+  b[x] = x == 0 ? 0 : (x == kLabels ? (int32_t)n : (int32_t)lo);
+}
+
+struct alignas(128) QHead {
+  unsigned long long v;
+  uint32_t pad[30];
+};
+
+template <int W, int T, int BT, int HUBW>
+__global__ __launch_bounds__(BT) void k_bu_chunks_xcd(
+    const int32_t* wl, int64_t nw, const int64_t* seg, const int64_t* P, const int32_t* owner,
+    const int32_t* col, const uint64_t* R, const uint64_t* alive, const uint64_t* gmask,
+    uint64_t* acc, const uint32_t* anyvis, int32_t filter_from, int xmode, QHead* heads) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G;
+  constexpr int BATCH = 2;  // chunks per dequeue
+  __shared__ int32_t tile[BT / 64][T];
+  __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
+  if constexpr (HUBW > 0) {
+    for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
+    __syncthreads();
+  }
+  const int lane = lane_id(), slot = lane % G;
+  int32_t* lst = tile[threadIdx.x >> 6];
+  V<VW> am;
 #pragma unroll
-    for (int j = 0; j < VW; ++j) g.w[j] = __shfl(g.w[j], slot);  // lane slot of sub-group 0
-    V<VW> unv, a = vzero<VW>();
-    bool lane_open = false;
-#pragma unroll
-    for (int j = 0; j < VW; ++j) {
-      unv.w[j] = ~r.w[j] & am.w[j];
-      lane_open |= (unv.w[j] & ~g.w[j]) != 0;
-    }
-    if (!__ballot(lane_open)) continue;  // wave-uniform
-    bool covered = false;
-    for (int64_t t0 = beg; t0 < lim && !covered; t0 += T) {
-      // ---- phase A: ids of this tile, filtered, compacted into lst[0..cnt)
-      constexpr int Q = T / 64;
-      int32_t u[Q];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int64_t e = t0 + q * 64 + lane;
-        u[q] = e < lim ? col[e] : -1;
-      }
-      if (!(xmode & 2)) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          bool vis;
-          if (HUBW > 0 && u[q] >= 0 && u[q] < HUBW * 32)
-            vis = (hub[u[q] >> 5] >> (u[q] & 31)) & 1u;
-          else
-            vis = u[q] < filter_from || any_visited(anyvis, u[q]);
-          if (u[q] >= 0 && !vis) u[q] = -1;
-        }
-      }
-      int cnt = 0;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const uint64_t m = __ballot(u[q] >= 0);
-        if (u[q] >= 0) lst[cnt + __popcll(m & lanemask_lt())] = u[q];
-        cnt += __popcll(m);
-      }
-      __builtin_amdgcn_wave_barrier();
-      // ---- phase B: rows of the surviving neighbours, 4 per lane group per step
-      for (int b = 0; b < cnt; b += PB * S) {
-        int32_t uu[PB];
-#pragma unroll
-        for (int q = 0; q < PB; ++q) {
-          const int k = b + q * S + sub;
-          uu[q] = k < cnt ? lst[k] : -1;
-        }
-#pragma unroll
-        for (int q = 0; q < PB; ++q)
-          if (uu[q] >= 0 && !(xmode & 1)) {
-            const V<VW> x = ldv<VW>(R + (int64_t)uu[q] * W + slot * VW);
-#pragma unroll
-            for (int j = 0; j < VW; ++j) a.w[j] |= x.w[j];
-          }
-#pragma unroll
-        for (int off = G; off < 64; off <<= 1)
-#pragma unroll
-          for (int j = 0; j < VW; ++j) a.w[j] |= __shfl_xor(a.w[j], off);
-        bool cov = true;
-#pragma unroll
-        for (int j = 0; j < VW; ++j) cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
-        if (!__ballot(!cov)) {
-          covered = true;
-          break;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();  // lst is rewritten by the next tile
-      // publish this chunk's bits so far and pick up the other chunks' (one round trip)
-      if (coop && !covered && t0 + T < lim) {
-        bool cov = true;
-        if (sub == 0) {
-#pragma unroll
-          for (int j = 0; j < VW; ++j) {
-            const uint64_t nb = a.w[j] & unv.w[j] & ~g.w[j];
-            g.w[j] |= nb ? atomicOr((unsigned long long*)&acc[vo + j], nb)
-                         : atomicOr((unsigned long long*)&acc[vo + j], 0ull);
-            g.w[j] |= nb;
-            cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
-          }
-        }
-        if (!__ballot(!cov)) covered = true;
-#pragma unroll
-        for (int j = 0; j < VW; ++j) g.w[j] = __shfl(g.w[j], slot);
-      }
-    }
-    if (sub == 0) {
-#pragma unroll
-      for (int j = 0; j < VW; ++j) {
-        const uint64_t nb = a.w[j] & unv.w[j] & ~g.w[j];
-        if (nb) atomicOr((unsigned long long*)&acc[vo + j], nb);
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  const int x0 = (int)(blockIdx.x % kLabels);
+  for (int k = 0; k < kLabels; ++k) {  // own range first, then steal
+    const int x = (x0 + k) % kLabels;
+    // Every value steering the loops is made wave-uniform (uni*): with a __shfl broadcast of
+    // the dequeued index the loops compiled as exec-masked "divergent" loops, and ROCm 7.2 turned
+    // the W <= 2 instantiations into loops that never ended.
+    const int64_t cbeg = x ? uni64(P[(int64_t)x * nw - 1]) : 0;
+    const int64_t ncx = uni64(P[(int64_t)(x + 1) * nw - 1]) - cbeg;
+    while (true) {
+      unsigned long long r = 0;
+      if (lane == 0) r = atomicAdd(&heads[x].v, (unsigned long long)BATCH);
+      const int64_t c0 = uni64((int64_t)r);
+      if (c0 >= ncx) break;
+      for (int q = 0; q < BATCH; ++q) {
+        const int64_t c = c0 + q;
+        if (c >= ncx) break;
+        const int64_t f = uni32(owner[cbeg + c]);
+        const int64_t i = f - (int64_t)x * nw;
+        const int32_t v = uni32(wl[i]);
+        const int64_t j0 = cbeg + c - (f ? uni64(P[f - 1]) : 0);
+        const int64_t beg = uni64(seg[f]) + j0 * kChunk;
+        const int64_t lim = min(uni64(seg[f + nw]), beg + (int64_t)kChunk);
+        chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, 0, xmode,
+                               lst);
       }
     }
   }
@@ -1134,6 +1292,8 @@ class BitparSolver final : public Solver {
     if (const char* t = getenv("MSBFS_TILE")) tile_ = atoi(t);
     if (const char* h = getenv("MSBFS_HUBLDS")) hub_lds_ = atoi(h);
     if (const char* f = getenv("MSBFS_FUSE_COUNT")) fuse_count_ = atoi(f);
+    if (const char* x = getenv("MSBFS_XCD")) xcd_ = atoi(x);
+    heads_.alloc(sizeof(QHead) * kLabels);
     MSBFS_HIP_CHECK(hipDeviceSynchronize());
   }
 
@@ -1281,6 +1441,19 @@ class BitparSolver final : public Solver {
 #undef MSBFS_BP_CASE
   }
 
+  LabelBounds label_bounds() {
+    if (lb_key_[0] != (const void*)g_.rowptr || lb_key_[1] != (const void*)g_.col) {
+      DevBuf d;
+      d.alloc(sizeof(int32_t) * (kLabels + 1));
+      k_label_bounds<<<1, 64>>>(g_.rowptr, n_eff(), d.as<int32_t>());
+      MSBFS_HIP_CHECK(hipGetLastError());
+      MSBFS_HIP_CHECK(hipMemcpy(lb_.b, d.p, sizeof(lb_.b), hipMemcpyDeviceToHost));
+      lb_key_[0] = g_.rowptr;
+      lb_key_[1] = g_.col;
+    }
+    return lb_;
+  }
+
   // 1 + the last vertex with deg > 0 (cached per graph buffers: relabelling replaces them).
   // Vertices beyond it are never active, never neighbours: level loops and clears skip them.
   int64_t n_eff() {
@@ -1325,6 +1498,13 @@ class BitparSolver final : public Solver {
   int fuse_count_ = 1;  // MSBFS_FUSE_COUNT=0: separate k_count_frontier pass
   int64_t n_eff_ = 0;
   const void* eff_key_[3] = {nullptr, nullptr, nullptr};
+  LabelBounds lb_{};
+  const void* lb_key_[2] = {nullptr, nullptr};
+  DevBuf segb_, segc_, segt_, heads_;
+  // MSBFS_XCD=1: first bottom-up level through XCD-labelled segments. Off: measured 2.7x slower
+  // on RMAT-26 (24.4 -> 65.6 ms for level 2) because cutting every wide row into 8 neighbour
+  // ranges multiplies the per-chunk overhead and the dequeue atomics (16M segments at wd = 32).
+  int xcd_ = 0;
 };
 
 // per-batch reset + sources + level 0 (k_init); leaves the loop state ready for level 1
@@ -1521,7 +1701,36 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         k_chunk_owner<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(offs_.as<int64_t>(), S.nactw,
                                                                    owner_.as<int32_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
-        if (hub_lds && (hub_lds_ & 1)) {
+        if (first_bu && xcd_ && g_.rows_sorted && S.nactw >= 1024 && n <= INT32_MAX) {
+          // first bottom-up level: XCD-labelled segment chunks (see k_bu_chunks_xcd)
+          const LabelBounds lb = label_bounds();
+          const int64_t nw = S.nactw, nf = (int64_t)kLabels * nw;
+          segb_.ensure((size_t)(nf + nw) * sizeof(int64_t));
+          segc_.ensure((size_t)nf * sizeof(int64_t) * 2);
+          const size_t tb = inclusive_scan_temp_bytes(nf);
+          segt_.ensure(tb);
+          owner_.ensure((size_t)(nf + S.ea / kChunk + kLabels + 1) * sizeof(int32_t));
+          int64_t* seg = segb_.as<int64_t>();
+          int64_t* cnt = segc_.as<int64_t>();
+          int64_t* P = cnt + nf;
+          k_seg_split<<<grid_for(nf + nw, kBlock, 8192), kBlock, 0, s>>>(
+              actw_[0].as<int32_t>(), nw, g_.rowptr, g_.col, lb, seg);
+          k_seg_counts<<<grid_for(nf, kBlock, 8192), kBlock, 0, s>>>(seg, nw, cnt);
+          inclusive_scan_i64(cnt, P, nf, segt_.p, segt_.bytes, s);
+          k_seg_owner<<<grid_for(nf, kBlock, 8192), kBlock, 0, s>>>(P, nf, owner_.as<int32_t>());
+          MSBFS_HIP_CHECK(hipMemsetAsync(heads_.p, 0, heads_.bytes, s));
+          MSBFS_HIP_CHECK(hipGetLastError());
+          if (hub_lds && (hub_lds_ & 1))
+            k_bu_chunks_xcd<W, 256, 1024, kHubW><<<512, 1024, 0, s>>>(
+                actw_[0].as<int32_t>(), nw, seg, P, owner_.as<int32_t>(), g_.col, R, alive,
+                sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, xmode_,
+                heads_.as<QHead>());
+          else
+            k_bu_chunks_xcd<W, 256, 1024, 0><<<512, 1024, 0, s>>>(
+                actw_[0].as<int32_t>(), nw, seg, P, owner_.as<int32_t>(), g_.col, R, alive,
+                sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, xmode_,
+                heads_.as<QHead>());
+        } else if (hub_lds && (hub_lds_ & 1)) {
           k_bu_chunks<W, 256, 1024, kHubW><<<grid_for(chunks_max, 16, 512), 1024, 0, s>>>(
               actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
               sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,

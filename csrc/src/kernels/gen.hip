@@ -178,6 +178,7 @@ void build_from_counts(DeviceGraph& g, DevBuf& cnt, hipStream_t s) {
   MSBFS_HIP_CHECK(hipGetLastError());
   g.own_col.alloc((size_t)std::max<int64_t>(nnz, 1) * sizeof(int32_t));
   g.col = g.own_col.as<int32_t>();
+  g.rows_sorted = false;
 }
 
 void alloc_rowptr(DeviceGraph& g, int64_t n) {
@@ -211,6 +212,7 @@ void device_graph_from_host(DeviceGraph& g, int64_t n, const int64_t* rowptr, co
   g.m = g.nnz / 2;
   g.own_col.alloc((size_t)std::max<int64_t>(g.nnz, 1) * sizeof(int32_t));
   g.col = g.own_col.as<int32_t>();
+  g.rows_sorted = false;
   MSBFS_HIP_CHECK(hipMemcpyAsync(g.rowptr, rowptr, (n + 1) * sizeof(int64_t),
                                  hipMemcpyHostToDevice, s));
   if (g.nnz)
@@ -371,7 +373,10 @@ void device_graph_sort_rows(DeviceGraph& g, hipStream_t s) {
   // Sorted rows make the device CSR deterministic (the atomic scatter is not) and give bottom-up
   // sweeps ascending-id neighbour order. Rows > 1024 are sorted with a segmented radix sort.
   const int64_t n = g.n;
-  if (n == 0) return;
+  if (n == 0) {
+    g.rows_sorted = true;
+    return;
+  }
   DevBuf lists((size_t)4 * n * sizeof(int32_t)), cnts(4 * sizeof(uint32_t));
   int32_t* small = lists.as<int32_t>();
   int32_t* mid = small + n;
@@ -421,6 +426,7 @@ void device_graph_sort_rows(DeviceGraph& g, hipStream_t s) {
     }
   }
   MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  g.rows_sorted = true;
 }
 
 // ---- frontier degree scan (shared by the level loops) ----------------------------------------
@@ -452,6 +458,20 @@ void frontier_degree_scan(const int64_t* rowptr, const int32_t* list, int64_t cn
   k_list_degrees<<<grid_for(cnt, kBlock), kBlock, 0, s>>>(rowptr, list, cnt, degs, chunk);
   MSBFS_HIP_CHECK(hipGetLastError());
   MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(t2, tb, degs, offs, (int)cnt, s));
+}
+
+size_t inclusive_scan_temp_bytes(int64_t max_items) {
+  size_t tb = 0;
+  MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, (int64_t*)nullptr,
+                                                   (int64_t*)nullptr, (int)std::max<int64_t>(max_items, 1)));
+  return tb + 256;
+}
+
+void inclusive_scan_i64(const int64_t* in, int64_t* out, int64_t cnt, void* temp,
+                        size_t temp_bytes, hipStream_t s) {
+  if (cnt <= 0) return;
+  if (cnt > INT32_MAX) fail("inclusive_scan_i64: more than 2^31 items");
+  MSBFS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, in, out, (int)cnt, s));
 }
 
 }  // namespace msbfs

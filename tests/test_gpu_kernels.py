@@ -123,12 +123,16 @@ def test_device_uniform_and_wrap(msbfs_pkg):
         assert np.array_equal(s.run(qs).F, m.cpu_bfs(hg, qs).F)
 
 
+@pytest.mark.parametrize("prep", ["none", "sorted"])
 @pytest.mark.parametrize("scale,K", [(16, 1024), (18, 700)])
-def test_bitpar_large_rmat_vs_cpu(msbfs_pkg, scale, K):
+def test_bitpar_large_rmat_vs_cpu(msbfs_pkg, scale, K, prep):
     """Large enough that every block runs many tiles and flushes its LDS queues repeatedly:
-    catches LDS init/flush races that 1-block toy graphs cannot."""
+    catches LDS init/flush races that 1-block toy graphs cannot. Sorted rows enable the
+    XCD-labelled segment chunks of the first bottom-up level (rows are binary-searched)."""
     m = msbfs_pkg
     dg = m.DeviceGraph.rmat(scale, 16, 3, device=0)
+    if prep == "sorted":
+        dg.sort_rows()
     qs = m.QuerySet.random(dg.n, K, 16, seed=scale)
     ref = m.cpu_bfs(dg.download(), qs, count_edges=True)
     with m.Solver(dg, "bitpar", max_groups=K) as s:
