@@ -45,6 +45,7 @@ constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr int kChunk = 1024;      // bottom-up edge chunk for wide vertices
 constexpr int kMaxGrid = 2048;    // blocks of the grid-stride level kernels
+constexpr int kSmallDeg = 64;     // max degree for the vertex-parallel top-down expansion
 
 template <int W>
 struct Lay {
@@ -386,19 +387,103 @@ __global__ __launch_bounds__(kBlock) void k_td_expand(
   q_flush(q, touched, &ctr->touched.v, 0, true);
 }
 
+// top-down expand for low-degree frontiers (road-like graphs: a few edges per vertex, thousands
+// of levels): G lanes per frontier vertex walk its row edge by edge. No degree prefix scan and no
+// per-edge binary search (k_td_expand's load balancing costs more than it saves when every
+// vertex has ~2-4 edges).
+// nf_dev (device-driven level batches): the frontier size written by the previous level's
+// finalize, read here instead of the host's nf_arg.
+template <int W, bool DIFF>
+__global__ __launch_bounds__(kBlock) void k_td_expand_small(
+    const int32_t* fl, int64_t nf_arg, const uint32_t* nf_dev, const int64_t* rowptr,
+    const int32_t* col, const uint64_t* visCur, const uint64_t* fsrc, const uint32_t* done,
+    uint64_t* accNext, int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  __shared__ LdsQueue q;
+  q_init(q);
+  __syncthreads();
+  const int64_t nf = nf_dev ? (int64_t)*nf_dev : nf_arg;
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nf; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t idx = tb + wv * VPW + sub;
+    int64_t e = 0, end = 0;
+    V<VW> fb = vzero<VW>();
+    if (idx < nf) {
+      const int32_t u = fl[idx];
+      e = rowptr[u];
+      end = rowptr[u + 1];
+      const int64_t uo = (int64_t)u * W + slot * VW;
+      if constexpr (DIFF) {
+        fb = ldv<VW>(visCur + uo);
+        const V<VW> old = ldv<VW>(fsrc + uo);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) fb.w[j] &= ~old.w[j];
+      } else {
+        fb = ldv<VW>(fsrc + uo);
+      }
+    }
+    // one edge per step for every vertex of the block (block-uniform steps, so the queue can
+    // flush every step; used only on graphs whose maximum degree is small)
+    while (__syncthreads_or(e < end)) {
+      bool touch = false;
+      int32_t v = 0;
+      if (e < end) {
+        v = col[e];
+        if (!is_done(done, v)) {
+          const int64_t vo = (int64_t)v * W + slot * VW;
+          const V<VW> r = ldv<VW>(visCur + vo);
+          bool any = false;
+#pragma unroll
+          for (int j = 0; j < VW; ++j) {
+            const uint64_t mm = fb.w[j] & ~r.w[j];
+            if (mm) {
+              atomicOr((unsigned long long*)&accNext[vo + j], mm);
+              any = true;
+            }
+          }
+          const uint64_t gm = (__ballot(any) >> (sub * G)) & L::GBITS;
+          if (gm && slot == 0) touch = atomicExch(&stamp[v], epoch) != epoch;
+        }
+        ++e;
+      }
+      q_push(q, touch, v);
+      q_flush(q, touched, &ctr->touched.v, TILE, false);
+    }
+  }
+  q_flush(q, touched, &ctr->touched.v, 0, true);
+}
+
+// device-driven level batch: seed slot 0 with the current frontier size and alive mask
+__global__ void k_batch_seed(Ctr* c0, uint32_t nf, const uint64_t* alive, uint64_t* alive0) {
+  if (threadIdx.x == 0) c0->fl2.v = nf;
+  if (threadIdx.x < 16) alive0[threadIdx.x] = alive[threadIdx.x];
+}
+
 // top-down finalize: new = acc & ~vis; update both visited buffers; build the next frontier.
-template <int W, bool COUNT>
+// FUSE: the level's new-bit counts go straight to this block's counter-slab row (as in the
+// bottom-up kernels) instead of a k_count_frontier pass over the new frontier.
+template <int W, bool COUNT, bool FUSE>
 __global__ __launch_bounds__(kBlock) void k_td_finalize(
     const int32_t* touched, const int64_t* rowptr, uint64_t* visCur, uint64_t* visOld,
     uint64_t* accNext, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* fl2,
-    Ctr* ctr, const int32_t* fl_old, int64_t nf_old,
-    uint64_t* accCur_zero, uint32_t* anyvis) {
+    Ctr* ctr, const int32_t* fl_old, int64_t nf_old_arg, const uint32_t* nfold_dev,
+    uint64_t* accCur_zero, uint32_t* anyvis, uint32_t* slabF) {
+  static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
+  const int64_t nf_old = nfold_dev ? (int64_t)*nfold_dev : nf_old_arg;
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ LdsQueue q;
   __shared__ unsigned long long scratch[kWaves];
+  __shared__ uint32_t cnt[FUSE ? 64 * W : 1];
+  if constexpr (FUSE)
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock) cnt[i] = 0;
   q_init(q);
   __syncthreads();
+  BitCounter<VW> bc;
+  int nadd = 0;
+  if constexpr (FUSE) bc.zero();
   const int64_t nt = ctr->touched.v;  // written by k_td_expand (previous kernel on the stream)
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
   const int wv = threadIdx.x >> 6;
@@ -435,6 +520,13 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
       stv<VW>(visOld + vo, nv);
       deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
     }
+    if constexpr (FUSE) {  // nw is zero for invalid lanes
+      bc.add(nw);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.spill(cnt, slot);
+        nadd = 0;
+      }
+    }
     const uint64_t bn = __ballot(anynew), bf = __ballot(notfull), br = __ballot(rnz);
     const bool g_new = (bn >> (sub * G)) & L::GBITS;
     const bool g_full = !((bf >> (sub * G)) & L::GBITS);
@@ -453,6 +545,12 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
   q_flush(q, fl2, &ctr->fl2.v, 0, true);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
+  if constexpr (FUSE) {
+    bc.spill(cnt, slot);
+    __syncthreads();
+    uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i];
+  }
   // zero the consumed top-down frontier bits of the previous frontier
   if (accCur_zero) {
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -1293,6 +1391,9 @@ class BitparSolver final : public Solver {
     if (const char* h = getenv("MSBFS_HUBLDS")) hub_lds_ = atoi(h);
     if (const char* f = getenv("MSBFS_FUSE_COUNT")) fuse_count_ = atoi(f);
     if (const char* x = getenv("MSBFS_XCD")) xcd_ = atoi(x);
+    if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
+    bctr_.alloc((size_t)(kBatch + 1) * (sizeof(Ctr) + 16 * sizeof(uint64_t)));
+    hbctr_ = std::make_unique<PinnedBuf>((size_t)(kBatch + 1) * sizeof(Ctr));
     heads_.alloc(sizeof(QHead) * kLabels);
     MSBFS_HIP_CHECK(hipDeviceSynchronize());
   }
@@ -1411,6 +1512,8 @@ class BitparSolver final : public Solver {
   template <int W, bool COUNT>
   void levels(Loop& S, RunStats* st, hipStream_t s);
   template <int W, bool COUNT>
+  void td_batch(Loop& S, RunStats* st, hipStream_t s);
+  template <int W, bool COUNT>
   void batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids, int64_t* F,
                   int64_t* edges2, RunStats* st, hipStream_t s);
   template <int W>
@@ -1505,6 +1608,13 @@ class BitparSolver final : public Solver {
   // on RMAT-26 (24.4 -> 65.6 ms for level 2) because cutting every wide row into 8 neighbour
   // ranges multiplies the per-chunk overhead and the dequeue atomics (16M segments at wd = 32).
   int xcd_ = 0;
+  // device-driven top-down level batches (low-degree graphs): up to kBatch levels per host
+  // round trip, doubling from 4 while the frontier lives (MSBFS_BATCH=1 turns them off)
+  static constexpr int kBatch = 64;
+  int batch_levels_ = kBatch;
+  int batch_next_ = 4;
+  DevBuf bctr_;  // (kBatch+1) Ctr slots, then (kBatch+1) x 16 alive words
+  std::unique_ptr<PinnedBuf> hbctr_;
 };
 
 // per-batch reset + sources + level 0 (k_init); leaves the loop state ready for level 1
@@ -1587,6 +1697,14 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       bottom_up = dirs_[S.level] == 'B';
     if (S.level < S.plan.size() && (S.plan[S.level] == 'T' || S.plan[S.level] == 'B'))
       bottom_up = S.plan[S.level] == 'B';
+    // low-degree graphs (road-like: thousands of small top-down levels): run a batch of levels
+    // without host round trips (kernels read the frontier sizes from device counters)
+    if (!bottom_up && batch_levels_ > 1 && g_.max_degree <= kSmallDeg && !trace &&
+        S.level + 2 < S.stop_level && opt.force_dir != 2 && S.plan.empty() &&
+        (dirs_.size() <= S.level)) {
+      td_batch<W, COUNT>(S, st, s);
+      continue;
+    }
     MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
     MSBFS_HIP_CHECK(hipMemsetAsync(sm.alive[S.alv ^ 1], 0, 16 * sizeof(uint64_t), s));
     ++S.level;
@@ -1598,9 +1716,25 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
     const uint64_t* alive = sm.alive[S.alv];
     if (!bottom_up) {
       // ---- top-down
+      ++epoch_;
+      if (g_.max_degree <= kSmallDeg) {
+        // low-degree graph: vertex-parallel expansion, no degree scan
+        const int eg = grid_for(S.nf, L::TILE, 4096);
+        if (S.fsrc_acc)
+          k_td_expand_small<W, false><<<eg, kBlock, 0, s>>>(
+              fl_[S.fc].as<int32_t>(), S.nf, nullptr, g_.rowptr, g_.col, R,
+              acc_[S.ac].as<uint64_t>(),
+              done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
+              touched_.as<int32_t>(), ctr_.as<Ctr>());
+        else
+          k_td_expand_small<W, true><<<eg, kBlock, 0, s>>>(
+              fl_[S.fc].as<int32_t>(), S.nf, nullptr, g_.rowptr, g_.col, R, O,
+              done_.as<uint32_t>(),
+              acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
+              touched_.as<int32_t>(), ctr_.as<Ctr>());
+      } else {
       frontier_degree_scan(g_.rowptr, fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(),
                            scan_tmp_.p, scan_bytes_, s);
-      ++epoch_;
       const int eg = grid_for(S.ef, L::TILE, 8192);
       if (S.fsrc_acc)
         k_td_expand<W, false><<<eg, kBlock, 0, s>>>(
@@ -1612,23 +1746,31 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
             fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R, O,
             done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
             touched_.as<int32_t>(), ctr_.as<Ctr>());
+      }
       MSBFS_HIP_CHECK(hipGetLastError());
       // touched <= min(n, frontier edges); the kernel reads the exact count from ctr
       const int64_t nt_max = std::min<int64_t>(std::max<int64_t>(S.ef, S.nf), n);
       const int gf = grid_for(nt_max, L::TILE, grid);
-      k_td_finalize<W, COUNT><<<gf, kBlock, 0, s>>>(
+      constexpr bool FUSE = !COUNT;
+      const bool fuse = FUSE && fuse_count_;
+      auto kf = fuse ? k_td_finalize<W, COUNT, FUSE> : k_td_finalize<W, COUNT, false>;
+      kf<<<gf, kBlock, 0, s>>>(
           touched_.as<int32_t>(), g_.rowptr, R, O, acc_[S.ac ^ 1].as<uint64_t>(), alive,
           sm.gmask, done_.as<uint32_t>(), fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
-          fl_[S.fc].as<int32_t>(), S.nf, S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr,
-          anyvis_.as<uint32_t>());
+          fl_[S.fc].as<int32_t>(), S.nf, nullptr,
+          S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr, anyvis_.as<uint32_t>(), slabF(rows));
       MSBFS_HIP_CHECK(hipGetLastError());
-      // new frontier bits are in acc_[ac ^ 1]
-      const int gc = grid_for(nt_max, L::TILE, grid);
-      k_count_frontier<W, COUNT, false><<<gc, kBlock, 0, s>>>(
-          fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), g_.rowptr, acc_[S.ac ^ 1].as<uint64_t>(),
-          nullptr, slabF(rows), slabE(rows));
-      rows += gc;
-      MSBFS_HIP_CHECK(hipGetLastError());
+      if (fuse) {
+        rows += gf;
+      } else {
+        // new frontier bits are in acc_[ac ^ 1]
+        const int gc = grid_for(nt_max, L::TILE, grid);
+        k_count_frontier<W, COUNT, false><<<gc, kBlock, 0, s>>>(
+            fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), g_.rowptr, acc_[S.ac ^ 1].as<uint64_t>(),
+            nullptr, slabF(rows), slabE(rows));
+        rows += gc;
+        MSBFS_HIP_CHECK(hipGetLastError());
+      }
       S.ac ^= 1;
       S.fsrc_acc = true;
       if (st) st->td_levels++;
@@ -1802,6 +1944,93 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
     S.alv ^= 1;
     if (st) st->levels++;
   }
+}
+
+// A batch of up to batch_next_ top-down levels with no host synchronisation: level i of the
+// batch reads its frontier size from counter slot i (slot 0 seeded from the host) and writes
+// slot i + 1; alive masks likewise. Levels after the frontier dies are no-ops (every kernel
+// sees a zero count). One copy of all slots afterwards restores the host's view.
+template <int W, bool COUNT>
+void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
+  using L = Lay<W>;
+  const int64_t n = g_.n;
+  const Small sm = small();
+  int K = std::min<int>(batch_next_, batch_levels_);
+  if (S.stop_level != 0xFFFFFFFFu) K = std::min<int64_t>(K, (int64_t)S.stop_level - S.level);
+  K = std::max(K, 1);
+  Ctr* slots = bctr_.as<Ctr>();
+  uint64_t* aslot = (uint64_t*)(slots + kBatch + 1);
+  MSBFS_HIP_CHECK(hipMemsetAsync(bctr_.p, 0, bctr_.bytes, s));
+  k_batch_seed<<<1, 64, 0, s>>>(slots, (uint32_t)S.nf, sm.alive[S.alv], aslot);
+  MSBFS_HIP_CHECK(hipGetLastError());
+  constexpr bool FUSE = !COUNT;
+  const bool fuse = FUSE && fuse_count_;
+  const int grid = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + L::TILE - 1) / L::TILE));
+  uint64_t* R = vis_[S.cur].as<uint64_t>();
+  uint64_t* O = vis_[S.cur ^ 1].as<uint64_t>();
+  const uint32_t level0 = S.level;
+  for (int i = 0; i < K; ++i) {
+    Ctr* prev = slots + i;
+    Ctr* cur = slots + i + 1;
+    const uint32_t level = level0 + 1 + i;
+    ++epoch_;
+    if (S.fsrc_acc)
+      k_td_expand_small<W, false><<<grid, kBlock, 0, s>>>(
+          fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v, g_.rowptr, g_.col, R,
+          acc_[S.ac].as<uint64_t>(), done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(),
+          stamp_.as<int32_t>(), epoch_, touched_.as<int32_t>(), cur);
+    else
+      k_td_expand_small<W, true><<<grid, kBlock, 0, s>>>(
+          fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v, g_.rowptr, g_.col, R, O,
+          done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
+          touched_.as<int32_t>(), cur);
+    auto kf = fuse ? k_td_finalize<W, COUNT, FUSE> : k_td_finalize<W, COUNT, false>;
+    kf<<<grid, kBlock, 0, s>>>(touched_.as<int32_t>(), g_.rowptr, R, O,
+                               acc_[S.ac ^ 1].as<uint64_t>(), aslot + 16 * i, sm.gmask,
+                               done_.as<uint32_t>(), fl_[S.fc ^ 1].as<int32_t>(), cur,
+                               fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v,
+                               S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr,
+                               anyvis_.as<uint32_t>(), slabF_.as<uint32_t>());
+    if (!fuse)
+      k_count_frontier<W, COUNT, false><<<grid, kBlock, 0, s>>>(
+          fl_[S.fc ^ 1].as<int32_t>(), cur, g_.rowptr, acc_[S.ac ^ 1].as<uint64_t>(), nullptr,
+          slabF_.as<uint32_t>(), slabE_.as<unsigned long long>());
+    const int rg = std::max(1, std::min(64, grid / 32));
+    const uint32_t weight = (level == 1 && !S.weight_l1) ? 0u : level;
+    k_level_reduce<W, COUNT><<<W * rg, kBlock, 0, s>>>(slabF_.as<uint32_t>(),
+                                                       slabE_.as<unsigned long long>(), grid, rg,
+                                                       sm.F, sm.E, aslot + 16 * (i + 1), weight);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    S.fc ^= 1;
+    S.ac ^= 1;
+    S.fsrc_acc = true;
+  }
+  // alive after the batch -> the host loop's current alive buffer
+  MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[S.alv], aslot + 16 * K, 16 * sizeof(uint64_t),
+                                 hipMemcpyDeviceToDevice, s));
+  MSBFS_HIP_CHECK(hipMemcpyAsync(hbctr_->p, bctr_.p, (size_t)(K + 1) * sizeof(Ctr),
+                                 hipMemcpyDeviceToHost, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  const Ctr* h = hbctr_->as<Ctr>();
+  int real = 0;
+  for (int i = 0; i < K; ++i) {
+    if (h[i].fl2.v == 0) break;  // frontier empty before level i: the rest were no-ops
+    ++real;
+    S.ev += (int64_t)h[i + 1].ev2.v;
+    if (level0 + 1 + i == 1) S.ev_l1 = S.ev;
+  }
+  S.level = level0 + real;
+  S.nf = h[real].fl2.v;
+  S.ef = (int64_t)h[real].ef2.v;
+  if (real < K && (K - real) % 2) {
+    // the no-op levels flipped the list / accumulator parity; only matters if the loop went on,
+    // which it does not (the frontier is empty)
+  }
+  if (st) {
+    st->td_levels += real;
+    st->levels += real;
+  }
+  batch_next_ = S.nf > 0 ? std::min(batch_next_ * 2, kBatch) : 4;
 }
 
 template <int W, bool COUNT>
