@@ -147,6 +147,7 @@ def main() -> int:
     dt = time.perf_counter() - t0
     dt = D.allreduce_max(dt, ctx)  # slowest rank
     ms = dt / max(1, args.steps) * 1e3
+    trace = solver.level_trace()  # last timed step: per-level direction and host wall time
     value = total_edges / (ms / 1e3) if ms > 0 else 0.0
     if ctx.rank == 0:
         out = {
@@ -174,6 +175,8 @@ def main() -> int:
                 "min_k": int(min_k) + 1, "min_f": int(min_f),
                 "levels": stats.get("levels"), "td_levels": stats.get("td_levels"),
                 "bu_levels": stats.get("bu_levels"), "batches": stats.get("batches"),
+                "dirs": "".join(t["dir"] for t in trace),
+                "level_ms": [round(t["ms"], 3) for t in trace],
                 "setup_s": round(setup_s, 3), "relabel": relabelled,
                 "candidates_ms": {k: round(v, 3) for k, v in cand_ms.items()},
             },

@@ -112,6 +112,7 @@ int main(int argc, char* argv[]) {
     auto comm = cpu ? std::move(world) : maybe_upgrade_rccl(std::move(world), a.comm, device);
 
     const auto t_pre0 = clk::now();  // main.cu:235
+    trace::push("preprocessing");
 
     // ---- graph: rank-0 load + broadcast, or per-rank deterministic generation -----------------
     HostCsr hg;
@@ -299,6 +300,7 @@ int main(int argc, char* argv[]) {
     }
 
     const auto t_pre1 = clk::now();  // main.cu:297-298
+    trace::pop();
     const double preprocessing_time = std::chrono::duration<double>(t_pre1 - t_pre0).count();
 
     // ---- computation (main.cu:301-400) ---------------------------------------------------------
@@ -312,6 +314,7 @@ int main(int argc, char* argv[]) {
     }
     for (int rep = 0; rep < a.repeat; ++rep) {
       comm->barrier();
+      trace::Range range_compute("computation");
       const auto t_c0 = clk::now();
       if (cpu) {
         HostCsr& g = hg;
@@ -324,9 +327,12 @@ int main(int argc, char* argv[]) {
         rs = RunStats();
         solver->hybrid_phase_a(K, q.off.data(), q.ids.data(), me, P, n_eff, me == 0, wbeg.data(),
                                hsend.as<uint64_t>(), hout.data(), &rs, stream);
-        comm->alltoallv_device_u64(hsend.as<uint64_t>(), scount, hrecv.as<uint64_t>(), rcount,
-                                   stream);
-        comm->allreduce_sum_i64(hout.data(), hout.size());
+        {
+          trace::Range range_x("hybrid exchange");
+          comm->alltoallv_device_u64(hsend.as<uint64_t>(), scount, hrecv.as<uint64_t>(), rcount,
+                                     stream);
+          comm->allreduce_sum_i64(hout.data(), hout.size());
+        }
         solver->hybrid_phase_c(K, wbeg[me], nw_me, P, n_eff, hrecv.as<uint64_t>(), hout.data(),
                                hF.data(), &rs, stream);
         for (int64_t i = 0; i < nlocal; ++i) F[i] = hout[local_to_global[i]] + hF[i];
@@ -394,7 +400,11 @@ int main(int argc, char* argv[]) {
                   << "\", \"traversed_edges\": " << std::setprecision(0) << edges
                   << ", \"teps\": " << std::setprecision(3) << (tmax > 0 ? edges / tmax : 0)
                   << ", \"levels\": " << rs.levels << ", \"td_levels\": " << rs.td_levels
-                  << ", \"bu_levels\": " << rs.bu_levels << ", \"F\": [";
+                  << ", \"bu_levels\": " << rs.bu_levels << ", \"dirs\": \"";
+        for (const LevelRec& r : rs.recs) std::cout << r.dir;
+        std::cout << "\", \"level_ms\": [" << std::setprecision(3);
+        for (size_t i = 0; i < rs.recs.size(); ++i) std::cout << (i ? ", " : "") << rs.recs[i].ms;
+        std::cout << "], \"F\": [";
         for (int64_t k = 0; k < K; ++k) std::cout << (k ? ", " : "") << allF[k];
         std::cout << "]}" << std::endl;
       }

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "msbfs/common.hpp"
+#include "msbfs/trace.hpp"
 
 #define MSBFS_HIP_CHECK(expr)                                                                \
   do {                                                                                       \
@@ -83,10 +84,12 @@ struct DeviceGraph {
   bool rows_sorted = false;
 };
 
-// Stats returned by solvers (mirrors msbfs_stats in msbfs.h).
+// Stats returned by solvers (mirrors msbfs_stats in msbfs.h). recs: one record per BFS level
+// (bit-parallel solver; see trace.hpp), exported by msbfs_solver_levels.
 struct RunStats {
   int64_t levels = 0, td_levels = 0, bu_levels = 0, batches = 0;
   double device_ms = 0;
+  std::vector<LevelRec> recs;
 };
 
 // ---- device-graph construction (kernels/gen.hip) -------------------------------------------

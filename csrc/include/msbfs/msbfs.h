@@ -32,6 +32,16 @@ typedef struct {
   double device_ms;
 } msbfs_stats;
 
+/* one BFS level of the last run (bit-parallel solver): direction 'T' (top-down push) or 'B'
+ * (bottom-up pull), union frontier size / degree sum entering the level, vertices newly visited
+ * by some group, bottom-up active (or top-down touched) vertices, host wall time of the level */
+typedef struct {
+  int32_t batch, level;
+  char dir, pad[3];
+  int64_t nf, ef, nf_next, active;
+  double ms;
+} msbfs_level;
+
 typedef struct {
   double alpha, beta;
   int wide_degree, force_dir, max_words;
@@ -99,6 +109,9 @@ int msbfs_solver_set_options(msbfs_solver s, const msbfs_options* o);
  * traversed-edge count). stream = hipStream_t or NULL for the null stream. */
 int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32_t* qids,
                      int64_t* F, int64_t* edges2, msbfs_stats* st, void* stream);
+/* per-level records of the solver's last run / hybrid phase: copies min(n, cap) records to out
+ * (nullable) and returns n (or -1 for a null solver) */
+int64_t msbfs_solver_levels(msbfs_solver s, msbfs_level* out, int64_t cap);
 void msbfs_solver_free(msbfs_solver s);
 
 /* ---- hybrid multi-GPU mode (bit-parallel solver) ----

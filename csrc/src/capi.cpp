@@ -18,6 +18,7 @@ struct msbfs_solver_s {
   int algo = 0;
   std::unique_ptr<msbfs::Solver> impl;
   int nthreads = 0;
+  std::vector<msbfs::LevelRec> recs;  // per-level records of the last run / phase
 };
 
 namespace {
@@ -50,8 +51,9 @@ hipStream_t as_stream(void* s) { return (hipStream_t)s; }
 
 // run fn on the solver's device stream with event timing and fill st
 template <class Fn>
-void timed(msbfs_solver s, void* stream, msbfs_stats* st, Fn&& fn) {
+void timed(msbfs_solver s, void* stream, msbfs_stats* st, const char* what, Fn&& fn) {
   MSBFS_HIP_CHECK(hipSetDevice(s->graph->g.device));
+  msbfs::trace::Range range(what);
   msbfs::RunStats rs;
   hipStream_t hs = as_stream(stream);
   hipEvent_t e0, e1;
@@ -65,6 +67,7 @@ void timed(msbfs_solver s, void* stream, msbfs_stats* st, Fn&& fn) {
   MSBFS_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  s->recs = std::move(rs.recs);
   if (st) {
     st->levels = rs.levels;
     st->td_levels = rs.td_levels;
@@ -376,7 +379,7 @@ int msbfs_solver_set_options(msbfs_solver s, const msbfs_options* o) {
 int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32_t* qids,
                      int64_t* F, int64_t* edges2, msbfs_stats* st, void* stream) {
   return guard([&] {
-    timed(s, stream, st, [&](msbfs::RunStats* rs, hipStream_t hs) {
+    timed(s, stream, st, "solver run", [&](msbfs::RunStats* rs, hipStream_t hs) {
       s->impl->run(K, qoff, qids, F, edges2, rs, hs);
     });
   });
@@ -395,7 +398,7 @@ int msbfs_solver_hybrid_phase_a(msbfs_solver s, int64_t K, const int64_t* qoff,
                                 int count_l1, const int32_t* wbeg, void* send_dev, int64_t* out,
                                 msbfs_stats* st, void* stream) {
   return guard([&] {
-    timed(s, stream, st, [&](msbfs::RunStats* rs, hipStream_t hs) {
+    timed(s, stream, st, "hybrid phase A", [&](msbfs::RunStats* rs, hipStream_t hs) {
       s->impl->hybrid_phase_a(K, qoff, qids, part, nparts, n_eff, count_l1 != 0, wbeg,
                               (uint64_t*)send_dev, out, rs, hs);
     });
@@ -406,11 +409,21 @@ int msbfs_solver_hybrid_phase_c(msbfs_solver s, int64_t K, int w_begin, int w_co
                                 int64_t n_eff, const void* recv_dev, const int64_t* reduced,
                                 int64_t* F_local, msbfs_stats* st, void* stream) {
   return guard([&] {
-    timed(s, stream, st, [&](msbfs::RunStats* rs, hipStream_t hs) {
+    timed(s, stream, st, "hybrid phase C", [&](msbfs::RunStats* rs, hipStream_t hs) {
       s->impl->hybrid_phase_c(K, w_begin, w_count, nparts, n_eff, (const uint64_t*)recv_dev,
                               reduced, F_local, rs, hs);
     });
   });
+}
+
+int64_t msbfs_solver_levels(msbfs_solver s, msbfs_level* out, int64_t cap) {
+  if (!s) return -1;
+  const int64_t n = (int64_t)s->recs.size();
+  for (int64_t i = 0; out && i < std::min(n, cap); ++i) {
+    const msbfs::LevelRec& r = s->recs[i];
+    out[i] = msbfs_level{r.batch, r.level, r.dir, {0, 0, 0}, r.nf, r.ef, r.nf_next, r.active, r.ms};
+  }
+  return n;
 }
 
 void msbfs_solver_free(msbfs_solver s) {

@@ -1703,11 +1703,13 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         S.level + 2 < S.stop_level && opt.force_dir != 2 && S.plan.empty() &&
         (dirs_.size() <= S.level)) {
       td_batch<W, COUNT>(S, st, s);
+      tl = std::chrono::steady_clock::now();
       continue;
     }
     MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
     MSBFS_HIP_CHECK(hipMemsetAsync(sm.alive[S.alv ^ 1], 0, 16 * sizeof(uint64_t), s));
     ++S.level;
+    trace::Range range_level(bottom_up ? "bitpar L%u BU" : "bitpar L%u TD", S.level);
     int rows = 0;  // slab rows written by this level's counting kernels
     auto slabF = [&](int r) { return slabF_.as<uint32_t>() + (size_t)r * 64 * W; };
     auto slabE = [&](int r) { return slabE_.as<unsigned long long>() + (size_t)r * 64 * W; };
@@ -1925,17 +1927,29 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       S.na = S.nact + S.nactw;
       S.ea = (int64_t)c.eu2;
     }
+    const auto t2 = std::chrono::steady_clock::now();
+    const double lms = std::chrono::duration<double, std::milli>(t2 - tl).count();
+    if (st) {
+      LevelRec rec;
+      rec.batch = (int32_t)st->batches;
+      rec.level = (int32_t)S.level;
+      rec.dir = bottom_up ? 'B' : 'T';
+      rec.nf = S.nf;
+      rec.ef = S.ef;
+      rec.nf_next = (int64_t)c.fl2;
+      rec.active = bottom_up ? S.na : (int64_t)c.touched;
+      rec.ms = lms;
+      st->recs.push_back(rec);
+    }
     if (trace) {
-      const auto t2 = std::chrono::steady_clock::now();
       fprintf(stderr,
               "[msbfs bp W=%d] level %u %s nf=%lld ef=%lld -> nf'=%lld ef'=%lld touched=%u "
               "active=%lld (wide %lld) ea=%lld ev=%lld  %.3f ms\n",
               W, S.level, bottom_up ? "BU" : "TD", (long long)S.nf, (long long)S.ef,
               (long long)c.fl2, (long long)c.ef2, c.touched, (long long)S.na, (long long)S.nactw,
-              (long long)S.ea, (long long)(S.ev + (long long)c.ev2),
-              std::chrono::duration<double, std::milli>(t2 - tl).count());
-      tl = t2;
+              (long long)S.ea, (long long)(S.ev + (long long)c.ev2), lms);
     }
+    tl = t2;
     S.nf = c.fl2;
     S.ef = (int64_t)c.ef2;
     S.ev += (int64_t)c.ev2;
@@ -1969,6 +1983,8 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
   uint64_t* R = vis_[S.cur].as<uint64_t>();
   uint64_t* O = vis_[S.cur ^ 1].as<uint64_t>();
   const uint32_t level0 = S.level;
+  const auto t0 = std::chrono::steady_clock::now();
+  trace::Range range_batch("bitpar L%u-%u TD batch", level0 + 1, level0 + K);
   for (int i = 0; i < K; ++i) {
     Ctr* prev = slots + i;
     Ctr* cur = slots + i + 1;
@@ -2025,6 +2041,22 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
   if (real < K && (K - real) % 2) {
     // the no-op levels flipped the list / accumulator parity; only matters if the loop went on,
     // which it does not (the frontier is empty)
+  }
+  if (st && real > 0) {  // per-level records; the batch's wall time is split evenly
+    const double ms = std::chrono::duration<double, std::milli>(
+                          std::chrono::steady_clock::now() - t0).count() / real;
+    for (int i = 0; i < real; ++i) {
+      LevelRec rec;
+      rec.batch = (int32_t)st->batches;
+      rec.level = (int32_t)(level0 + 1 + i);
+      rec.dir = 'T';
+      rec.nf = h[i].fl2.v;
+      rec.ef = (int64_t)h[i].ef2.v;
+      rec.nf_next = h[i + 1].fl2.v;
+      rec.active = h[i + 1].touched.v;
+      rec.ms = ms;
+      st->recs.push_back(rec);
+    }
   }
   if (st) {
     st->td_levels += real;

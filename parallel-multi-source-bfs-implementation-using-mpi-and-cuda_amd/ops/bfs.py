@@ -63,6 +63,18 @@ class Solver:
                 C.byref(st), C.c_void_p(stream) if stream else None))
         return BfsResult(F, None if E is None else E // 2, st.as_dict())
 
+    def level_trace(self) -> list:
+        """Per-level records of the last run / hybrid phase (bit-parallel solver): batch, level,
+        dir ('T' push / 'B' pull), frontier size nf and degree sum ef entering the level, newly
+        visited vertices nf_next, active (bottom-up) or touched (top-down) vertices, host ms."""
+        L = native.lib()
+        n = int(L.msbfs_solver_levels(self._h, None, 0))
+        if n <= 0:
+            return []
+        buf = (native.Level * n)()
+        L.msbfs_solver_levels(self._h, buf, n)
+        return [r.as_dict() for r in buf]
+
     # ---- hybrid multi-GPU mode (parallel/hybrid.py drives these) ----
     def hybrid_max_groups(self) -> int:
         return int(native.lib().msbfs_solver_hybrid_max_groups(self._h))

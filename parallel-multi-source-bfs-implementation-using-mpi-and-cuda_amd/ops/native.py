@@ -39,6 +39,18 @@ class Stats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class Level(C.Structure):
+    """One BFS level of a solver run (msbfs_level in msbfs.h)."""
+    _fields_ = [("batch", C.c_int32), ("level", C.c_int32), ("dir", C.c_char),
+                ("pad", C.c_char * 3), ("nf", C.c_int64), ("ef", C.c_int64),
+                ("nf_next", C.c_int64), ("active", C.c_int64), ("ms", C.c_double)]
+
+    def as_dict(self):
+        return {"batch": self.batch, "level": self.level, "dir": self.dir.decode(),
+                "nf": self.nf, "ef": self.ef, "nf_next": self.nf_next, "active": self.active,
+                "ms": self.ms}
+
+
 class Options(C.Structure):
     _fields_ = [("alpha", C.c_double), ("beta", C.c_double), ("wide_degree", C.c_int),
                 ("force_dir", C.c_int), ("max_words", C.c_int)]
@@ -87,6 +99,7 @@ def _sig(lib):
         "msbfs_solver_set_options": (C.c_int, [vp, P(Options)]),
         "msbfs_solver_run": (C.c_int, [vp, C.c_int64, i64p, i32p, i64p, i64p, P(Stats), vp]),
         "msbfs_solver_free": (None, [vp]),
+        "msbfs_solver_levels": (C.c_int64, [vp, P(Level), C.c_int64]),
         "msbfs_argmin": (C.c_int64, [i64p, C.c_int64]),
         "msbfs_hybrid_extent": (C.c_int, [vp, i64p]),
         "msbfs_solver_hybrid_max_groups": (C.c_int64, [vp]),

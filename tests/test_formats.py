@@ -127,3 +127,11 @@ def test_csr_cache(tmp_path, msbfs_pkg):
     os.utime(p, (1, 1))
     c = m.Graph.from_file(p, use_cache=True)
     assert c.m == 256 * 5
+
+
+def test_level_record_layout():
+    """ctypes mirror of msbfs_level (msbfs.h) has the C layout: 2 x i32, char + pad, 4 x i64, f64."""
+    import ctypes as C
+    from msbfs.ops import native
+    assert C.sizeof(native.Level) == 56
+    assert native.Level.nf.offset == 16 and native.Level.ms.offset == 48

@@ -166,3 +166,21 @@ def test_relabelled_graph_same_answers(msbfs_pkg, algo):
         res = s.run(qs, count_edges=True)
     assert np.array_equal(res.F, ref.F)
     assert np.array_equal(res.edges, ref.edges)
+
+
+def test_bitpar_level_trace(msbfs_pkg):
+    """Per-level records (msbfs_solver_levels): one per level, consistent with the stats and with
+    the frontier chain (the next level starts from the previous level's new vertices)."""
+    m = msbfs_pkg
+    for g in (m.Graph.rmat(12, 16, 3), m.Graph.grid(60, 60, 0.9, 0, 2)):
+        qs = m.QuerySet.random(g.n, 100, 4, seed=5)
+        with m.Solver(g.to_device(0), "bitpar", max_groups=qs.K) as s:
+            r = s.run(qs)
+            tr = s.level_trace()
+        assert len(tr) == r.stats["levels"]
+        assert sum(t["dir"] == "B" for t in tr) == r.stats["bu_levels"]
+        assert sum(t["dir"] == "T" for t in tr) == r.stats["td_levels"]
+        assert [t["level"] for t in tr] == list(range(1, len(tr) + 1))
+        for a, b in zip(tr, tr[1:]):
+            assert b["nf"] == a["nf_next"]
+        assert tr[-1]["nf_next"] == 0 and all(t["ms"] >= 0 for t in tr)

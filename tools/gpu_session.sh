@@ -74,6 +74,13 @@ for s in "$@"; do
            step rmat_a14 600 python tools/bench_graph.py --graph rmat:24:16 --groups 1024 --relabel 1 ;;
     rmat22) step rmat22 300 python bench.py --scale 22 --groups 64 --steps 5 --warmup 1 --verify 16 ;;
     usaroad) step usaroad 900 python tools/bench_graph.py --graph grid:4896:4896:0.6 --groups 64 --steps 1 ;;
+    hyb8trace) MSBFS_TRACE=1 step hyb8trace 600 python tools/hybrid_sim.py --scale 26 --ranks 8 --no-roundrobin ;;
+    hyb4trace) MSBFS_TRACE=1 step hyb4trace 600 python tools/hybrid_sim.py --scale 26 --ranks 4 --no-roundrobin ;;
+    pmcnarrow) export TMPDIR=/tmp
+         step pmcn1 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_bu_narrow" --output-format csv -d gpurun_out/pmcn1 -o run -- python bench.py --steps 1 --warmup 0 --groups 128
+         step pmcn2 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_VALU --kernel-include-regex "k_bu_narrow" --output-format csv -d gpurun_out/pmcn2 -o run -- python bench.py --steps 1 --warmup 0 --groups 128
+         step pmcn3 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum --kernel-include-regex "k_bu_narrow" --output-format csv -d gpurun_out/pmcn3 -o run -- python bench.py --steps 1 --warmup 0 --groups 128
+         ;;
     hybsimall) step hybsimall 900 python tools/hybrid_sim.py --scale 26 --ranks 2 4 8 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
