@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 
 #include "msbfs/device.hpp"
@@ -180,7 +181,7 @@ __device__ __forceinline__ void slab_store(Lds<W, COUNT>& s, uint32_t* slabF,
 // LDS atomic per set bit in a divergent loop. Spilled to LDS every < 2^D additions.
 template <int VW>
 struct BitCounter {
-  static constexpr int D = 7;
+  static constexpr int D = 6;
   uint64_t c[VW][D];
   __device__ __forceinline__ void zero() {
 #pragma unroll
@@ -609,6 +610,53 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Sparse row codes for the first bottom-up level. Its frontier is the level-1 frontier: outside
+// the top hubs a vertex there was reached from one or two sources, so its visited row (8*W bytes)
+// mostly holds a single set bit (RMAT-26, 1024 groups: ~1.2 bits per row below degree ~9K).
+// Gathering those rows made the level bound by Infinity-Cache traffic (rocprofv3, k_bu_chunks at
+// level 2: 44 % L2 hit rate, ~115 GB of L2 misses for 0.74e9 row gathers). code[u] (16 bit):
+// 0 = row empty, 1 + g = only group g set, kDenseCode = anything else (gathered as before). The
+// frontier's codes occupy a 64x smaller footprint than its rows, so the pulls mostly hit L2.
+// Only ids >= code_from use codes: after degree relabelling the lower ids are the hubs, whose rows
+// are dense and L2-resident. The codes live in the top-down touched buffer (unused by bottom-up
+// levels, rebuilt by every top-down level).
+// ---------------------------------------------------------------------------------------------
+constexpr uint16_t kDenseCode = 0xFFFF;
+constexpr int32_t kNoCodes = INT32_MAX;
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_build_codes(const uint64_t* R, const uint32_t* anyvis,
+                                                        int64_t lo, int64_t hi, uint16_t* code) {
+  for (int64_t u = lo + (int64_t)blockIdx.x * kBlock + threadIdx.x; u < hi;
+       u += (int64_t)gridDim.x * kBlock) {
+    uint16_t c = 0;
+    if (any_visited(anyvis, (int32_t)u)) {
+      int pc = 0, first = 0;
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const uint64_t w = R[u * W + j];
+        if (w && pc == 0) first = j * 64 + __ffsll((unsigned long long)w) - 1;
+        pc += __popcll(w);
+      }
+      c = pc == 0 ? 0 : (pc == 1 ? (uint16_t)(1 + first) : kDenseCode);
+    }
+    code[u] = c;
+  }
+}
+
+// first id with degree < min_deg (rows relabelled by descending degree; one thread)
+__global__ void k_degree_bound(const int64_t* rowptr, int64_t n, int64_t min_deg, int32_t* out) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rowptr[mid + 1] - rowptr[mid] < min_deg) hi = mid;
+    else lo = mid + 1;
+  }
+  *out = (int32_t)lo;
+}
+
+
+// ---------------------------------------------------------------------------------------------
 // bottom-up, narrow vertices: G lanes per vertex, early exit when every alive group is covered.
 // Each step takes C = 8 neighbours: the group's G lanes load and filter them cooperatively
 // (8/G column ids + 8/G bitmap probes per lane instead of 8 + 8), then every lane pulls its
@@ -654,24 +702,45 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
   BitCounter<VW> bc;
   int nadd = 0;
   if constexpr (FUSE) bc.zero();
-  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nact; tb += (int64_t)gridDim.x * TILE) {
-    const int64_t idx = tb + wv * VPW + sub;
+  // Software pipeline over the grid-stride tiles: the active-list entry is loaded two tiles
+  // ahead and the vertex's visited row and row offsets one tile ahead, so a tile starts with
+  // its column loads instead of two dependent round trips (list entry -> row / offsets).
+  const int64_t stride = (int64_t)gridDim.x * TILE, lofs = wv * VPW + sub;
+  int64_t tb = (int64_t)blockIdx.x * TILE;
+  int32_t v1 = 0, v2 = 0;  // list entries of tiles tb and tb + stride
+  V<VW> r1 = vzero<VW>();  // row of v1
+  int64_t b1 = 0;          // row offsets of v1
+  uint32_t d1 = 0;
+  if (tb + lofs < nact) v1 = act[tb + lofs];
+  if (tb + stride + lofs < nact) v2 = act[tb + stride + lofs];
+  if (tb + lofs < nact) {
+    r1 = ldv<VW>(R + (int64_t)v1 * W + slot * VW);
+    b1 = rowptr[v1];
+    d1 = (uint32_t)(rowptr[v1 + 1] - b1);
+  }
+  for (; tb < nact; tb += stride) {
+    const int64_t idx = tb + lofs;
     const bool valid = idx < nact;
-    int32_t v = 0;
-    V<VW> r = vzero<VW>(), unv = vzero<VW>(), acc = vzero<VW>();
+    const int32_t v = valid ? v1 : 0;
+    const V<VW> r = r1;
+    const int64_t beg = b1, end = b1 + d1;
+    // prefetch: row / offsets of the next tile, list entry of the one after
+    v1 = v2;
+    if (idx + stride < nact) {
+      r1 = ldv<VW>(R + (int64_t)v1 * W + slot * VW);
+      b1 = rowptr[v1];
+      d1 = (uint32_t)(rowptr[v1 + 1] - b1);
+    }
+    if (idx + 2 * stride < nact) v2 = act[idx + 2 * stride];
+    V<VW> unv = vzero<VW>(), acc = vzero<VW>();
     bool lane_open = false, rnz = false;
-    int64_t beg = 0, end = 0;
     if (valid) {
-      v = act[idx];
-      r = ldv<VW>(R + (int64_t)v * W + slot * VW);
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
         unv.w[j] = ~r.w[j] & am.w[j];
         lane_open |= unv.w[j] != 0;
         rnz |= r.w[j] != 0;
       }
-      beg = rowptr[v];
-      end = rowptr[v + 1];
     }
     const bool g_open = valid && ((__ballot(lane_open) >> (sub * G)) & L::GBITS);
     if (g_open) {
@@ -793,7 +862,8 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
                                            const uint64_t* R, const V<Lay<W>::VW>& am,
                                            uint64_t* acc, const uint32_t* anyvis,
                                            const uint32_t* hub, int32_t filter_from, int coop,
-                                           int xmode, int32_t* lst) {
+                                           int xmode, int32_t* lst, const uint16_t* code,
+                                           int32_t code_from, unsigned long long* wacc) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
   constexpr int PB = 8;  // rows in flight per lane group in phase B
@@ -841,6 +911,24 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
           vis = u[q] < filter_from || any_visited(anyvis, u[q]);
         if (u[q] >= 0 && !vis) u[q] = -1;
       }
+    }
+    if (code_from != kNoCodes) {  // wave-uniform
+      // single-group neighbours: their bit goes into this wave's LDS words (ds_or_b64) instead
+      // of a row gather; the words are folded into every lane group's accumulator below
+      if (lane < W) wacc[lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      uint32_t cd[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) cd[q] = u[q] >= code_from ? code[u[q]] : kDenseCode;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (cd[q] != kDenseCode) {
+          if (cd[q]) atomicOr(&wacc[(cd[q] - 1) >> 6], 1ull << ((cd[q] - 1) & 63));
+          u[q] = -1;
+        }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < VW; ++j) a.w[j] |= wacc[slot * VW + j];
     }
     int cnt = 0;
 #pragma unroll
@@ -909,10 +997,12 @@ template <int W, int T, int BT, int HUBW>
 __global__ __launch_bounds__(BT) void k_bu_chunks(
     const int32_t* wl, int64_t nw, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, const uint64_t* alive, const uint64_t* gmask, uint64_t* acc,
-    const uint32_t* anyvis, int32_t filter_from, int coop, int xmode, const int32_t* owner) {
+    const uint32_t* anyvis, int32_t filter_from, int coop, int xmode, const int32_t* owner,
+    const uint16_t* code, int32_t code_from) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G;
   __shared__ int32_t tile[BT / 64][T];
+  __shared__ unsigned long long wacc[BT / 64][W];
   __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
   if constexpr (HUBW > 0) {
     for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
@@ -942,7 +1032,7 @@ __global__ __launch_bounds__(BT) void k_bu_chunks(
     const int64_t beg = uni64(rowptr[v]) + j0 * kChunk;
     const int64_t lim = min(uni64(rowptr[v + 1]), beg + (int64_t)kChunk);
     chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop, xmode,
-                           lst);
+                           lst, code, code_from, wacc[threadIdx.x >> 6]);
   }
 }
 
@@ -1038,6 +1128,7 @@ __global__ __launch_bounds__(BT) void k_bu_chunks_xcd(
   constexpr int VW = L::VW, G = L::G;
   constexpr int BATCH = 2;  // chunks per dequeue
   __shared__ int32_t tile[BT / 64][T];
+  __shared__ unsigned long long wacc[BT / 64][W];
   __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
   if constexpr (HUBW > 0) {
     for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
@@ -1071,7 +1162,7 @@ __global__ __launch_bounds__(BT) void k_bu_chunks_xcd(
         const int64_t beg = uni64(seg[f]) + j0 * kChunk;
         const int64_t lim = min(uni64(seg[f + nw]), beg + (int64_t)kChunk);
         chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, 0, xmode,
-                               lst);
+                               lst, nullptr, kNoCodes, wacc[threadIdx.x >> 6]);
       }
     }
   }
@@ -1391,6 +1482,8 @@ class BitparSolver final : public Solver {
     if (const char* h = getenv("MSBFS_HUBLDS")) hub_lds_ = atoi(h);
     if (const char* f = getenv("MSBFS_FUSE_COUNT")) fuse_count_ = atoi(f);
     if (const char* x = getenv("MSBFS_XCD")) xcd_ = atoi(x);
+    if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
+    if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
     bctr_.alloc((size_t)(kBatch + 1) * (sizeof(Ctr) + 16 * sizeof(uint64_t)));
     hbctr_ = std::make_unique<PinnedBuf>((size_t)(kBatch + 1) * sizeof(Ctr));
@@ -1489,6 +1582,7 @@ class BitparSolver final : public Solver {
     bool weight_l1 = true;              // add level-1 counts to F
     std::string plan;                   // plan[level] = 'T'/'B' forces the next level
     int64_t ev_l1 = 0;                  // ev after level 1
+    int64_t ef0 = 0;                    // degree sum of the sources (level-0 frontier)
   };
   struct Small {
     unsigned long long* F;
@@ -1608,6 +1702,34 @@ class BitparSolver final : public Solver {
   // on RMAT-26 (24.4 -> 65.6 ms for level 2) because cutting every wide row into 8 neighbour
   // ranges multiplies the per-chunk overhead and the dequeue atomics (16M segments at wd = 32).
   int xcd_ = 0;
+  // sparse row codes on the first bottom-up level (MSBFS_CODES=0: off); ids with degree >=
+  // code_deg_ * nnz / (source degree sum), i.e. expected >= code_deg_ set bits, keep row gathers
+  int codes_ = 1;
+  double code_deg_ = 2.0;
+  std::map<int64_t, int32_t> code_bound_;
+  const void* code_key_[2] = {nullptr, nullptr};
+  // first id with degree < min_deg (rounded to a power of two, cached per graph); 0 when the
+  // graph keeps the user's ids (no degree order to exploit)
+  int32_t code_bound(double min_deg) {
+    if (!g_.old2new) return 0;
+    if (code_key_[0] != (const void*)g_.rowptr || code_key_[1] != (const void*)g_.col) {
+      code_bound_.clear();
+      code_key_[0] = g_.rowptr;
+      code_key_[1] = g_.col;
+    }
+    int64_t d = 1;
+    while (d < (int64_t)min_deg && d < ((int64_t)1 << 40)) d <<= 1;
+    auto it = code_bound_.find(d);
+    if (it != code_bound_.end()) return it->second;
+    DevBuf b;
+    b.alloc(sizeof(int32_t));
+    k_degree_bound<<<1, 1>>>(g_.rowptr, g_.n, d, b.as<int32_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+    int32_t h = 0;
+    MSBFS_HIP_CHECK(hipMemcpy(&h, b.p, sizeof(h), hipMemcpyDeviceToHost));
+    code_bound_[d] = h;
+    return h;
+  }
   // device-driven top-down level batches (low-degree graphs): up to kBatch levels per host
   // round trip, doubling from 4 while the frontier lives (MSBFS_BATCH=1 turns them off)
   static constexpr int kBatch = 64;
@@ -1672,6 +1794,7 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
   const HostCtr c = read_ctr(s);  // also retires the pinned/host source copies
   S.nf = c.fl2;
   S.ef = (int64_t)c.ef2;
+  S.ef0 = S.ef;
   S.ev = (int64_t)c.ev2;
   S.na = n;
   S.ea = g_.nnz;  // active estimate before the first bottom-up build
@@ -1803,6 +1926,23 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       const bool filter = (double)S.ev < filter_frac_ * (double)g_.nnz;
+      // sparse row codes for the first bottom-up level after level 1 (see k_build_codes)
+      int32_t code_from = kNoCodes;
+      const uint16_t* codes = nullptr;
+      if (first_bu && S.level == 2 && codes_ && W >= 8 && S.ef0 > 0 && n <= INT32_MAX) {
+        const int64_t ne = n_eff();
+        code_from = (int32_t)std::min<int64_t>(
+            code_bound(code_deg_ * (double)g_.nnz / (double)S.ef0), ne);
+        if (code_from < ne) {
+          uint16_t* cb = touched_.as<uint16_t>() ;  // 4n bytes >= 2n
+          k_build_codes<W><<<grid_for(ne - code_from, kBlock, 8192), kBlock, 0, s>>>(
+              R, anyvis_.as<uint32_t>(), code_from, ne, cb);
+          MSBFS_HIP_CHECK(hipGetLastError());
+          codes = cb;
+        } else {
+          code_from = kNoCodes;
+        }
+      }
       // hub rows (lowest ids after degree relabelling) sized to ~hub_bytes_ are always loaded
       const int64_t hub_ids = g_.old2new ? (int64_t)(hub_bytes_ / (8.0 * W)) : 0;
       const int32_t filter_from =
@@ -1878,14 +2018,14 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           k_bu_chunks<W, 256, 1024, kHubW><<<grid_for(chunks_max, 16, 512), 1024, 0, s>>>(
               actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
               sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-              first_bu ? 0 : 1, xmode_, owner_.as<int32_t>());
+              first_bu ? 0 : 1, xmode_, owner_.as<int32_t>(), codes, code_from);
         } else {
           auto ck = tile_ >= 1024 ? k_bu_chunks<W, 1024, kBlock, 0>
                     : tile_ >= 512 ? k_bu_chunks<W, 512, kBlock, 0> : k_bu_chunks<W, 256, kBlock, 0>;
           ck<<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
               actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
               sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-              first_bu ? 0 : 1, xmode_, owner_.as<int32_t>());
+              first_bu ? 0 : 1, xmode_, owner_.as<int32_t>(), codes, code_from);
         }
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(S.nactw, L::TILE, grid);
