@@ -993,12 +993,37 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
   }
 }
 
+// Chunk descriptor: vertex, first column position, edge count (<= kChunk). Built once per level
+// by k_chunk_desc; a wave reads its next descriptor with one scalar load while it pulls the
+// current chunk (vs an owner -> list entry -> row offsets chain of dependent loads per chunk).
+struct ChunkDesc {
+  int32_t v;
+  uint32_t beg_lo, beg_hi;
+  int32_t len;
+};
+
+__global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl, int64_t nw,
+                                                       const int64_t* offs, const int64_t* rowptr,
+                                                       ChunkDesc* desc) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int32_t v = wl[i];
+    const int64_t b = rowptr[v], e = rowptr[v + 1];
+    const int64_t c0 = i ? offs[i - 1] : 0, c1 = offs[i];
+    for (int64_t c = c0; c < c1; ++c) {
+      const int64_t cb = b + (c - c0) * kChunk;
+      desc[c] = ChunkDesc{v, (uint32_t)cb, (uint32_t)((uint64_t)cb >> 32),
+                          (int32_t)min((int64_t)kChunk, e - cb)};
+    }
+  }
+}
+
 template <int W, int T, int BT, int HUBW>
 __global__ __launch_bounds__(BT) void k_bu_chunks(
-    const int32_t* wl, int64_t nw, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
-    const uint64_t* R, const uint64_t* alive, const uint64_t* gmask, uint64_t* acc,
-    const uint32_t* anyvis, int32_t filter_from, int coop, int xmode, const int32_t* owner,
-    const uint16_t* code, int32_t code_from) {
+    const ChunkDesc* __restrict__ desc, const int64_t* nchunks_p, const int32_t* col,
+    const uint64_t* R,
+    const uint64_t* alive, const uint64_t* gmask, uint64_t* acc, const uint32_t* anyvis,
+    int32_t filter_from, int coop, int xmode, const uint16_t* code, int32_t code_from) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G;
   __shared__ int32_t tile[BT / 64][T];
@@ -1010,7 +1035,7 @@ __global__ __launch_bounds__(BT) void k_bu_chunks(
   }
   const int slot = lane_id() % G;
   int32_t* lst = tile[threadIdx.x >> 6];
-  const int64_t nchunks = uni64(offs[nw - 1]);
+  const int64_t nchunks = uni64(*nchunks_p);  // inclusive chunk prefix of the last wide vertex
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   V<VW> am;
@@ -1020,17 +1045,16 @@ __global__ __launch_bounds__(BT) void k_bu_chunks(
   // is covered) chunks are dealt round robin over the waves, which balances the hubs' expensive
   // chunks. With early exit a wave takes a contiguous run, so a vertex's later chunks usually
   // come after its earlier ones have published their bits and are skipped at the first check.
-  // owner[c] = index of chunk c's vertex in wl: one load instead of a ~20-step dependent binary
-  // search over offs.
   const int64_t cstart = uni64(coop ? nchunks * wave / nwaves : wave);
   const int64_t cend = uni64(coop ? nchunks * (wave + 1) / nwaves : nchunks);
   const int64_t cstep = uni64(coop ? 1 : nwaves);
+  ChunkDesc d{0, 0, 0, 0};
+  if (cstart < cend) d = desc[cstart];
   for (int64_t c = cstart; c < cend; c += cstep) {
-    const int64_t i = uni32(owner[c]);
-    const int32_t v = uni32(wl[i]);
-    const int64_t j0 = c - (i ? uni64(offs[i - 1]) : 0);
-    const int64_t beg = uni64(rowptr[v]) + j0 * kChunk;
-    const int64_t lim = min(uni64(rowptr[v + 1]), beg + (int64_t)kChunk);
+    const int32_t v = uni32(d.v);
+    const int64_t beg = uni64((int64_t)(((uint64_t)d.beg_hi << 32) | d.beg_lo));
+    const int64_t lim = beg + uni32(d.len);
+    if (c + cstep < cend) d = desc[c + cstep];  // next descriptor, in flight during the pull
     chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop, xmode,
                            lst, code, code_from, wacc[threadIdx.x >> 6]);
   }
@@ -1681,7 +1705,7 @@ class BitparSolver final : public Solver {
   const DeviceGraph& g_;
   int maxW_ = 1;
   DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
-      ctr_, small_, pairs_, slabF_, slabE_, anyvis_, owner_;
+      ctr_, small_, pairs_, slabF_, slabE_, anyvis_, owner_, desc_;
   double filter_frac_ = 0.5;  // skip unvisited neighbours while visited edges < frac * nnz
   double hub_bytes_ = 0.0;    // MSBFS_HUB_MB: hub rows loaded without the bitmap test (off: best)
   size_t scan_bytes_ = 0;
@@ -1981,11 +2005,15 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         frontier_degree_scan(g_.rowptr, actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(),
                              scan_tmp_.p, scan_bytes_, s, kChunk);
         const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
-        owner_.ensure((size_t)chunks_max * sizeof(int32_t));
-        k_chunk_owner<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(offs_.as<int64_t>(), S.nactw,
-                                                                   owner_.as<int32_t>());
-        MSBFS_HIP_CHECK(hipGetLastError());
-        if (first_bu && xcd_ && g_.rows_sorted && S.nactw >= 1024 && n <= INT32_MAX) {
+        const bool use_xcd = first_bu && xcd_ && g_.rows_sorted && S.nactw >= 1024 && n <= INT32_MAX;
+        if (!use_xcd) {
+          desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
+          k_chunk_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
+              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr,
+              desc_.as<ChunkDesc>());
+          MSBFS_HIP_CHECK(hipGetLastError());
+        }
+        if (use_xcd) {
           // first bottom-up level: XCD-labelled segment chunks (see k_bu_chunks_xcd)
           const LabelBounds lb = label_bounds();
           const int64_t nw = S.nactw, nf = (int64_t)kLabels * nw;
@@ -2015,17 +2043,16 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                 sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, xmode_,
                 heads_.as<QHead>());
         } else if (hub_lds && (hub_lds_ & 1)) {
+          // exact chunk count = offs[nactw - 1], read on the device (no host round trip)
           k_bu_chunks<W, 256, 1024, kHubW><<<grid_for(chunks_max, 16, 512), 1024, 0, s>>>(
-              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
-              sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-              first_bu ? 0 : 1, xmode_, owner_.as<int32_t>(), codes, code_from);
+              desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(),
+              anyvis_.as<uint32_t>(), filter_from, first_bu ? 0 : 1, xmode_, codes, code_from);
         } else {
           auto ck = tile_ >= 1024 ? k_bu_chunks<W, 1024, kBlock, 0>
                     : tile_ >= 512 ? k_bu_chunks<W, 512, kBlock, 0> : k_bu_chunks<W, 256, kBlock, 0>;
           ck<<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
-              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col, R, alive,
-              sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-              first_bu ? 0 : 1, xmode_, owner_.as<int32_t>(), codes, code_from);
+              desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(),
+              anyvis_.as<uint32_t>(), filter_from, first_bu ? 0 : 1, xmode_, codes, code_from);
         }
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(S.nactw, L::TILE, grid);
