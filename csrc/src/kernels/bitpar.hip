@@ -718,12 +718,19 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
     b1 = rowptr[v1];
     d1 = (uint32_t)(rowptr[v1 + 1] - b1);
   }
+  int32_t u1[Q];  // first-step column ids of the current tile's vertex (third pipeline stage)
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    u1[q] = (tb + lofs < nact && (uint32_t)(q * G + slot) < d1) ? col[b1 + q * G + slot] : -1;
   for (; tb < nact; tb += stride) {
     const int64_t idx = tb + lofs;
     const bool valid = idx < nact;
     const int32_t v = valid ? v1 : 0;
     const V<VW> r = r1;
     const int64_t beg = b1, end = b1 + d1;
+    int32_t u0[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) u0[q] = u1[q];
     // prefetch: row / offsets of the next tile, list entry of the one after
     v1 = v2;
     if (idx + stride < nact) {
@@ -749,7 +756,7 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
           const int64_t ee = e + q * G + slot;
-          u[q] = ee < end ? col[ee] : -1;
+          u[q] = e == beg ? u0[q] : (ee < end ? col[ee] : -1);  // first step: preloaded
         }
         // ids below filter_from are loaded without a probe (filter off: filter_from = INT_MAX)
 #pragma unroll
@@ -816,6 +823,10 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
         ev += deg;
       }
     }
+    // third stage: the next tile's first-step ids (its offsets arrived during this tile)
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      u1[q] = (idx + stride < nact && (uint32_t)(q * G + slot) < d1) ? col[b1 + q * G + slot] : -1;
     q_push(qa, keep && (int)deg <= next_wide, v);
     q_push(qw, keep && (int)deg > next_wide, v);
     q_push(qf, app, v);
