@@ -668,8 +668,8 @@ __global__ void k_degree_bound(const int64_t* rowptr, int64_t n, int64_t min_deg
 // FUSE: the level's new-bit counts are accumulated here (register bit-sliced counters -> LDS ->
 // this block's row of the counter slab, slabF = first row of this launch) instead of by a
 // separate k_count_frontier pass that re-reads both rows of every new frontier vertex.
-template <int W, bool COUNT, int BT, int HUBW, bool FUSE>
-__global__ __launch_bounds__(BT) void k_bu_narrow(
+template <int W, bool COUNT, int BT, int HUBW, bool FUSE, bool FILT = true>
+__global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
@@ -759,14 +759,25 @@ __global__ __launch_bounds__(BT) void k_bu_narrow(
           u[q] = e == beg ? u0[q] : (ee < end ? col[ee] : -1);  // first step: preloaded
         }
         // ids below filter_from are loaded without a probe (filter off: filter_from = INT_MAX)
+        // probes: every load first, every use after (with the use next to the load inside the
+        // branch the compiler waited for each probe before issuing the next)
+        if (FILT && filter_from != INT32_MAX) {  // wave-uniform
+          // (LDS and global results in separate registers: a shared destination made the LDS
+          // read wait for the outstanding global probes)
+          uint32_t pg[Q], ph[Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          if (u[q] >= filter_from) {
-            bool vis;
-            if (HUBW > 0 && u[q] < HUBW * 32) vis = (hub[u[q] >> 5] >> (u[q] & 31)) & 1u;
-            else vis = any_visited(anyvis, u[q]);
-            if (!vis) u[q] = -1;
+          for (int q = 0; q < Q; ++q) {
+            pg[q] = ~0u;
+            if (u[q] >= filter_from && !(HUBW > 0 && u[q] < HUBW * 32)) pg[q] = anyvis[u[q] >> 5];
           }
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            ph[q] = ~0u;
+            if (HUBW > 0 && u[q] >= filter_from && u[q] < HUBW * 32) ph[q] = hub[u[q] >> 5];
+          }
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (!(((pg[q] & ph[q]) >> (u[q] & 31)) & 1u)) u[q] = -1;
         }
         V<VW> x[C];
 #pragma unroll
@@ -877,7 +888,7 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
                                            int32_t code_from, unsigned long long* wacc) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
-  constexpr int PB = 8;  // rows in flight per lane group in phase B
+  constexpr int PB = VW == 2 ? 4 : 8;  // rows in flight per lane group in phase B
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
   const int64_t vo = (int64_t)v * W + slot * VW;
   const V<VW> r = ldv<VW>(R + vo);
@@ -912,16 +923,22 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
       const int64_t e = t0 + q * 64 + lane;
       u[q] = e < lim ? col[e] : -1;
     }
-    if (!(xmode & 2)) {
+    if (!(xmode & 2) && filter_from != INT32_MAX) {
+      // probes: every load first, every use after (see k_bu_narrow)
+      uint32_t pg[Q], ph[Q];  // separate destinations (see k_bu_narrow)
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        bool vis;
-        if (HUBW > 0 && u[q] >= 0 && u[q] < HUBW * 32)
-          vis = (hub[u[q] >> 5] >> (u[q] & 31)) & 1u;
-        else
-          vis = u[q] < filter_from || any_visited(anyvis, u[q]);
-        if (u[q] >= 0 && !vis) u[q] = -1;
+        pg[q] = ~0u;
+        if (u[q] >= filter_from && !(HUBW > 0 && u[q] < HUBW * 32)) pg[q] = anyvis[u[q] >> 5];
       }
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        ph[q] = ~0u;
+        if (HUBW > 0 && u[q] >= 0 && u[q] < HUBW * 32) ph[q] = hub[u[q] >> 5];
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (u[q] >= 0 && !(((pg[q] & ph[q]) >> (u[q] & 31)) & 1u)) u[q] = -1;
     }
     if (code_from != kNoCodes) {  // wave-uniform
       // single-group neighbours: their bit goes into this wave's LDS words (ds_or_b64) instead
@@ -930,7 +947,10 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
       __builtin_amdgcn_wave_barrier();
       uint32_t cd[Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) cd[q] = u[q] >= code_from ? code[u[q]] : kDenseCode;
+      for (int q = 0; q < Q; ++q) {
+        cd[q] = kDenseCode;
+        if (u[q] >= code_from) cd[q] = code[u[q]];
+      }
 #pragma unroll
       for (int q = 0; q < Q; ++q)
         if (cd[q] != kDenseCode) {
@@ -957,13 +977,19 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
         const int k = b + q * S + sub;
         uu[q] = k < cnt ? lst[k] : -1;
       }
+      if (!(xmode & 1)) {
+        // loads first, ORs after: the compiler then keeps all PB loads in flight
+        V<VW> x[PB];
 #pragma unroll
-      for (int q = 0; q < PB; ++q)
-        if (uu[q] >= 0 && !(xmode & 1)) {
-          const V<VW> x = ldv<VW>(R + (int64_t)uu[q] * W + slot * VW);
-#pragma unroll
-          for (int j = 0; j < VW; ++j) a.w[j] |= x.w[j];
+        for (int q = 0; q < PB; ++q) {
+          x[q] = vzero<VW>();
+          if (uu[q] >= 0) x[q] = ldv<VW>(R + (int64_t)uu[q] * W + slot * VW);
         }
+#pragma unroll
+        for (int q = 0; q < PB; ++q)
+#pragma unroll
+          for (int j = 0; j < VW; ++j) a.w[j] |= x[q].w[j];
+      }
 #pragma unroll
       for (int off = G; off < 64; off <<= 1)
 #pragma unroll
@@ -1030,7 +1056,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl, int64_
 }
 
 template <int W, int T, int BT, int HUBW>
-__global__ __launch_bounds__(BT) void k_bu_chunks(
+__global__ __launch_bounds__(BT, BT >= 1024 ? 8 : 1) void k_bu_chunks(
     const ChunkDesc* __restrict__ desc, const int64_t* nchunks_p, const int32_t* col,
     const uint64_t* R,
     const uint64_t* alive, const uint64_t* gmask, uint64_t* acc, const uint32_t* anyvis,
@@ -2001,8 +2027,12 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           if (fuse) rows += gn;
         } else {
           const int gn = grid_for(S.nact, L::TILE, grid);
-          auto kn = fuse ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE>
-                         : k_bu_narrow<W, COUNT, kBlock, 0, false>;
+          // FILT = false: no probe code at all (fewer VGPRs) on the levels that load every row
+          const bool filt = filter_from != INT32_MAX;
+          auto kn = fuse ? (filt ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, true>
+                                 : k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false>)
+                         : (filt ? k_bu_narrow<W, COUNT, kBlock, 0, false, true>
+                                 : k_bu_narrow<W, COUNT, kBlock, 0, false, false>);
           kn<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
                                    sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                    fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),

@@ -184,3 +184,23 @@ def test_bitpar_level_trace(msbfs_pkg):
         for a, b in zip(tr, tr[1:]):
             assert b["nf"] == a["nf_next"]
         assert tr[-1]["nf_next"] == 0 and all(t["ms"] >= 0 for t in tr)
+
+
+@pytest.mark.parametrize("K", [300, 1024])
+def test_bitpar_sparse_codes_relabelled(msbfs_pkg, K, monkeypatch):
+    """First bottom-up level with sparse single-group row codes (k_build_codes) on a degree-
+    relabelled device RMAT graph: identical F with the codes on, off, and against the CPU oracle."""
+    m = msbfs_pkg
+    g = m.DeviceGraph.rmat(14, 16, 5, device=0)
+    qs = m.QuerySet.random(g.n, K, 8, seed=K)
+    ref = m.cpu_bfs(g.download(), qs)  # original ids (download() after relabelling is internal)
+    g.relabel_by_degree()
+    out = {}
+    for codes in ("1", "0"):
+        monkeypatch.setenv("MSBFS_CODES", codes)
+        monkeypatch.setenv("MSBFS_CODE_DEG", "0.5")  # codes for most ids, dense fallback exercised
+        with m.Solver(g, "bitpar", max_groups=K) as s:
+            out[codes] = s.run(qs).F
+    assert np.array_equal(out["1"], ref.F)
+    assert np.array_equal(out["0"], ref.F)
+    g.close()
