@@ -49,6 +49,23 @@ std::vector<std::string> split(const std::string& s, char d) {
   return out;
 }
 
+// Fault injection for the failure-handling tests (the reference has none: a rank-0 exit() leaves
+// the other ranks blocked in MPI_Bcast, main.cu:95-99). MSBFS_FAULT=<where>:<rank>
+// makes rank <rank> throw at <where> in {load, compute}; every failure on any rank then takes
+// the whole job down (MPI_Abort / ncclCommAbort) instead of leaving peers in a collective.
+void maybe_inject(const char* where, int rank) {
+  static const char* spec = getenv("MSBFS_FAULT");
+  if (!spec) return;
+  const std::string s(spec);
+  const size_t c = s.find(':');
+  if (s.substr(0, c) != where) return;
+  if (c != std::string::npos && atoi(s.c_str() + c + 1) != rank) return;
+  fail(std::string("injected fault: ") + where + " on rank " + std::to_string(rank));
+}
+
+// the communicator a failure must abort (world until the RCCL upgrade, then the upgraded one)
+Comm* g_active = nullptr;
+
 int algo_id(const std::string& a) {
   if (a == "auto") return 0;
   if (a == "bitpar") return 1;
@@ -64,6 +81,7 @@ int algo_id(const std::string& a) {
 int main(int argc, char* argv[]) {
   auto world = make_world_comm(&argc, &argv);
   const int world_rank = world->rank();
+  g_active = world.get();
 
   if (argc < 5) {  // main.cu:204-212
     if (world_rank == 0)
@@ -91,6 +109,7 @@ int main(int argc, char* argv[]) {
     else if (!strcmp(argv[i], "--sort-rows")) a.sort_rows = true;
   }
 
+  std::unique_ptr<Comm> comm;  // outlives the try block: the catch may have to abort it
   try {
     if (a.numGPU <= 0) fail("-gn must be >= 1 (the reference divides by it, main.cu:227)");
     const int algo = algo_id(a.algo);
@@ -109,10 +128,12 @@ int main(int argc, char* argv[]) {
       }
       MSBFS_HIP_CHECK(hipSetDevice(device));
     }
-    auto comm = cpu ? std::move(world) : maybe_upgrade_rccl(std::move(world), a.comm, device);
+    comm = cpu ? std::move(world) : maybe_upgrade_rccl(std::move(world), a.comm, device);
+    g_active = comm.get();
 
     const auto t_pre0 = clk::now();  // main.cu:235
     trace::push("preprocessing");
+    maybe_inject("load", comm->rank());
 
     // ---- graph: rank-0 load + broadcast, or per-rank deterministic generation -----------------
     HostCsr hg;
@@ -341,6 +362,7 @@ int main(int argc, char* argv[]) {
         solver->run(nlocal, local.off.data(), local.ids.data(), F.data(), a.json ? E2.data() : nullptr,
                     &rs, stream);
       }
+      maybe_inject("compute", comm->rank());
       // packed (F << qbits | q) min-reduce keeps the lowest-index tie-break (main.cu:391-396)
       int qbits = 1;
       while ((int64_t(1) << qbits) <= K) ++qbits;
@@ -413,6 +435,10 @@ int main(int argc, char* argv[]) {
     comm.reset();
   } catch (const std::exception& e) {
     fprintf(stderr, "msbfs: %s\n", e.what());
+    fflush(stderr);
+    // peers may be blocked in a collective: abort the job rather than finalize (MPI_Finalize
+    // would wait for them forever)
+    if (g_active && g_active->size() > 1) g_active->abort(EXIT_FAILURE);
     finalize_world();
     return EXIT_FAILURE;
   }

@@ -108,3 +108,20 @@ def test_python_cli_matches(tmp_path, msbfs_pkg):
     assert lines[2] == "Query number (k) with minimum F value: 2" and lines[3] == "Minimum F value: 3"
     r = _run([sys.executable, "-m", "msbfs", "-g"], {"PYTHONPATH": ROOT})
     assert r.returncode == 255 and "Usage" in r.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+@pytest.mark.parametrize("fault", ["load:0", "load:2", "compute:1"])
+def test_cli_fault_takes_job_down(tmp_path, msbfs_pkg, fault):
+    """A failure on any rank ends the whole job promptly with an error (MPI_Abort), instead of
+    leaving the other ranks blocked in a collective as the reference's rank-0 exit() does
+    (main.cu:95-99). MSBFS_FAULT=<where>:<rank> injects the failure."""
+    cli = _cli(msbfs_pkg)
+    rank = fault.split(":")[1]
+    r = subprocess.run([MPIEXEC, "-n", "3", "-errfile-pattern", str(tmp_path / "err.%r"), cli,
+                        "--gen", "rmat:9:8:2", "--qgen", "20:3:5", "-gn", "1", "--algo", "cpu"],
+                       capture_output=True, text=True, timeout=60,
+                       env={**os.environ, "MSBFS_FAULT": fault})
+    assert r.returncode != 0
+    err = (tmp_path / f"err.{rank}").read_text()
+    assert f"injected fault: {fault.split(':')[0]} on rank {rank}" in err
