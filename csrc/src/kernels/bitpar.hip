@@ -1056,7 +1056,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl, int64_
 }
 
 template <int W, int T, int BT, int HUBW>
-__global__ __launch_bounds__(BT, BT >= 1024 ? 8 : 1) void k_bu_chunks(
+__global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_bu_chunks(
     const ChunkDesc* __restrict__ desc, const int64_t* nchunks_p, const int32_t* col,
     const uint64_t* R,
     const uint64_t* alive, const uint64_t* gmask, uint64_t* acc, const uint32_t* anyvis,
@@ -1544,6 +1544,7 @@ class BitparSolver final : public Solver {
     if (const char* f = getenv("MSBFS_FUSE_COUNT")) fuse_count_ = atoi(f);
     if (const char* x = getenv("MSBFS_XCD")) xcd_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
+    if (const char* x = getenv("MSBFS_HUBBIG")) hub_big_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
     bctr_.alloc((size_t)(kBatch + 1) * (sizeof(Ctr) + 16 * sizeof(uint64_t)));
@@ -1766,6 +1767,7 @@ class BitparSolver final : public Solver {
   // sparse row codes on the first bottom-up level (MSBFS_CODES=0: off); ids with degree >=
   // code_deg_ * nnz / (source degree sum), i.e. expected >= code_deg_ set bits, keep row gathers
   int codes_ = 1;
+  int hub_big_ = 3;  // MSBFS_HUBBIG: bit 0 narrow, bit 1 chunks use a 128-KB LDS hub bitmap
   double code_deg_ = 2.0;
   std::map<int64_t, int32_t> code_bound_;
   const void* code_key_[2] = {nullptr, nullptr};
@@ -2017,8 +2019,14 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         if (hub_lds && (hub_lds_ & 2)) {
           constexpr int BT = 1024;
           const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
-          auto kn = fuse ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE>
-                         : k_bu_narrow<W, COUNT, BT, kHubW, false>;
+          // the narrow kernel runs one 1024-thread block per CU anyway (VGPR-bound), so its LDS
+          // has room for a 4x larger hub bitmap (MSBFS_HUBBIG bit 0)
+          constexpr int kHubBig = 32768;  // 128 KB: ids < 1M
+          const bool big = (hub_big_ & 1) && n > (int64_t)kHubBig * 32 * 4;
+          auto kn = fuse ? (big ? k_bu_narrow<W, COUNT, BT, kHubBig, FUSE>
+                                : k_bu_narrow<W, COUNT, BT, kHubW, FUSE>)
+                         : (big ? k_bu_narrow<W, COUNT, BT, kHubBig, false>
+                                : k_bu_narrow<W, COUNT, BT, kHubW, false>);
           kn<<<gn, BT, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
                                sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
@@ -2085,9 +2093,14 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                 heads_.as<QHead>());
         } else if (hub_lds && (hub_lds_ & 1)) {
           // exact chunk count = offs[nactw - 1], read on the device (no host round trip)
-          k_bu_chunks<W, 256, 1024, kHubW><<<grid_for(chunks_max, 16, 512), 1024, 0, s>>>(
-              desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(),
-              anyvis_.as<uint32_t>(), filter_from, first_bu ? 0 : 1, xmode_, codes, code_from);
+          // MSBFS_HUBBIG bit 1: one block per CU with a 128-KB hub bitmap (ids < 1M)
+          constexpr int kHubBig = 32768;
+          const bool big = (hub_big_ & 2) && n > (int64_t)kHubBig * 32 * 4;
+          auto ck = big ? k_bu_chunks<W, 256, 1024, kHubBig> : k_bu_chunks<W, 256, 1024, kHubW>;
+          ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
+              desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
+              sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
+              first_bu ? 0 : 1, xmode_, codes, code_from);
         } else {
           auto ck = tile_ >= 1024 ? k_bu_chunks<W, 1024, kBlock, 0>
                     : tile_ >= 512 ? k_bu_chunks<W, 512, kBlock, 0> : k_bu_chunks<W, 256, kBlock, 0>;
