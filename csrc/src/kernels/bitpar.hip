@@ -657,6 +657,48 @@ __global__ void k_degree_bound(const int64_t* rowptr, int64_t n, int64_t min_deg
 
 
 // ---------------------------------------------------------------------------------------------
+// Prefix pull + tail push for the first bottom-up level (rows sorted by id, degree relabelled).
+// The LDS hub bitmap covers the ids < H; a pull that scanned whole rows had to probe the global
+// visited bitmap for every neighbour id >= H (the degree tail: ~40 % of the edge endpoints on
+// RMAT-26, almost none of them in the level-1 frontier). Instead the pulls stop at the first id
+// >= H, and the few level-1 frontier vertices u >= H push their bits to their neighbours here:
+// acc[v] |= row(u) (atomicOr, mostly one word thanks to the sparse codes) and stamp[v] = epoch.
+// The narrow pull folds acc[v] of stamped vertices into its accumulator (and clears it); wide
+// vertices collect it with their chunk results in k_bu_wide_finalize. Sources need no push:
+// every neighbour of a source was reached at level 1. Only own vertices (v % nparts == part) are
+// targets (the hybrid mode's level 2 pulls only those), and done vertices are skipped, so every
+// written acc entry is consumed and cleared within the level.
+// ---------------------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_push_tail(
+    const int32_t* fl, int64_t nf, int32_t H, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, const uint16_t* code, int32_t code_from, const uint32_t* done,
+    int part, int nparts, uint64_t* acc, int32_t* stamp, int32_t epoch) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nf;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int32_t u = fl[i];
+    if (u < H) continue;
+    const uint32_t c = (code && u >= code_from) ? code[u] : kDenseCode;
+    if (c == 0) continue;
+    const int64_t b = rowptr[u], e = rowptr[u + 1];
+    for (int64_t k = b; k < e; ++k) {
+      const int32_t v = col[k];
+      if (nparts > 1 && v % nparts != part) continue;
+      if (is_done(done, v)) continue;
+      if (c != kDenseCode) {
+        atomicOr((unsigned long long*)&acc[(int64_t)v * W + ((c - 1) >> 6)], 1ull << ((c - 1) & 63));
+      } else {
+        for (int j = 0; j < W; ++j) {
+          const uint64_t w = R[(int64_t)u * W + j];
+          if (w) atomicOr((unsigned long long*)&acc[(int64_t)v * W + j], (unsigned long long)w);
+        }
+      }
+      stamp[v] = epoch;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // bottom-up, narrow vertices: G lanes per vertex, early exit when every alive group is covered.
 // Each step takes C = 8 neighbours: the group's G lanes load and filter them cooperatively
 // (8/G column ids + 8/G bitmap probes per lane instead of 8 + 8), then every lane pulls its
@@ -668,12 +710,17 @@ __global__ void k_degree_bound(const int64_t* rowptr, int64_t n, int64_t min_deg
 // FUSE: the level's new-bit counts are accumulated here (register bit-sliced counters -> LDS ->
 // this block's row of the counter slab, slabF = first row of this launch) instead of by a
 // separate k_count_frontier pass that re-reads both rows of every new frontier vertex.
-template <int W, bool COUNT, int BT, int HUBW, bool FUSE, bool FILT = true>
+// PFX (prefix-pull level, see k_push_tail): rows are scanned only up to the first id >= HUBW*32,
+// and pushed bits (acc of vertices with stamp == epoch) seed the accumulator.
+template <int W, bool COUNT, int BT, int HUBW, bool FUSE, bool FILT = true, bool PFX = false>
 __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
-    int next_wide, uint32_t* slabF) {
+    int next_wide, uint32_t* slabF, uint64_t* pacc = nullptr, const int32_t* stamp = nullptr,
+    int32_t epoch = 0) {
+  static_assert(!PFX || HUBW > 0, "the prefix pull relies on the LDS hub bitmap");
+  constexpr int32_t H = HUBW * 32;
   static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
@@ -749,6 +796,12 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
         rnz |= r.w[j] != 0;
       }
     }
+    if constexpr (PFX) {  // bits pushed from the tail frontier (k_push_tail)
+      if (valid && stamp[v] == epoch) {
+        acc = ldv<VW>(pacc + (int64_t)v * W + slot * VW);
+        stv<VW>(pacc + (int64_t)v * W + slot * VW, vzero<VW>());
+      }
+    }
     const bool g_open = valid && ((__ballot(lane_open) >> (sub * G)) & L::GBITS);
     if (g_open) {
       for (int64_t e = beg; e < end; e += C) {
@@ -757,6 +810,15 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
         for (int q = 0; q < Q; ++q) {
           const int64_t ee = e + q * G + slot;
           u[q] = e == beg ? u0[q] : (ee < end ? col[ee] : -1);  // first step: preloaded
+        }
+        bool past = false;  // PFX: this step reached the row's ids >= H (sorted rows)
+        if constexpr (PFX) {
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (u[q] >= H) {
+              u[q] = -1;
+              past = true;
+            }
         }
         // ids below filter_from are loaded without a probe (filter off: filter_from = INT_MAX)
         // probes: every load first, every use after (with the use next to the load inside the
@@ -795,6 +857,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
         }
         // the whole group runs this loop in lock step (same v); exit when all lanes covered
         if (!((__ballot(!cov) >> (sub * G)) & L::GBITS)) break;
+        if (PFX && ((__ballot(past) >> (sub * G)) & L::GBITS)) break;
       }
     }
     V<VW> nw;
@@ -1039,13 +1102,41 @@ struct ChunkDesc {
   int32_t len;
 };
 
+// first position in the sorted row [b, e) whose id is >= H
+__device__ __forceinline__ int64_t row_lower_bound(const int32_t* col, int64_t b, int64_t e,
+                                                   int32_t H) {
+  while (b < e) {
+    const int64_t mid = (b + e) >> 1;
+    if (col[mid] < H) b = mid + 1;
+    else e = mid;
+  }
+  return b;
+}
+
+// chunk counts of the wide vertices' row prefixes with ids < H (prefix-pull level, see
+// k_push_tail); inclusive-scanned into offs by the host
+__global__ __launch_bounds__(kBlock) void k_prefix_chunks(const int32_t* wl, int64_t nw,
+                                                          const int64_t* rowptr, const int32_t* col,
+                                                          int32_t H, int64_t* cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int32_t v = wl[i];
+    const int64_t b = rowptr[v];
+    cnt[i] = (row_lower_bound(col, b, rowptr[v + 1], H) - b + kChunk - 1) / kChunk;
+  }
+}
+
+// H < INT32_MAX: chunks cover only the row prefix with ids < H (rows sorted)
 __global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl, int64_t nw,
                                                        const int64_t* offs, const int64_t* rowptr,
+                                                       const int32_t* col, int32_t H,
                                                        ChunkDesc* desc) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
        i += (int64_t)gridDim.x * kBlock) {
     const int32_t v = wl[i];
-    const int64_t b = rowptr[v], e = rowptr[v + 1];
+    const int64_t b = rowptr[v];
+    int64_t e = rowptr[v + 1];
+    if (H != INT32_MAX) e = row_lower_bound(col, b, e, H);
     const int64_t c0 = i ? offs[i - 1] : 0, c1 = offs[i];
     for (int64_t c = c0; c < c1; ++c) {
       const int64_t cb = b + (c - c0) * kChunk;
@@ -1545,6 +1636,7 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_XCD")) xcd_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
     if (const char* x = getenv("MSBFS_HUBBIG")) hub_big_ = atoi(x);
+    if (const char* x = getenv("MSBFS_PFX")) pfx_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
     bctr_.alloc((size_t)(kBatch + 1) * (sizeof(Ctr) + 16 * sizeof(uint64_t)));
@@ -1767,6 +1859,7 @@ class BitparSolver final : public Solver {
   // sparse row codes on the first bottom-up level (MSBFS_CODES=0: off); ids with degree >=
   // code_deg_ * nnz / (source degree sum), i.e. expected >= code_deg_ set bits, keep row gathers
   int codes_ = 1;
+  int pfx_ = 1;      // MSBFS_PFX=0: first bottom-up level pulls whole rows (no tail push)
   int hub_big_ = 3;  // MSBFS_HUBBIG: bit 0 narrow, bit 1 chunks use a 128-KB LDS hub bitmap
   double code_deg_ = 2.0;
   std::map<int64_t, int32_t> code_bound_;
@@ -2015,13 +2108,39 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       // counting fused into the traversal kernels (the edge-count pass keeps k_count_frontier)
       constexpr bool FUSE = !COUNT;
       const bool fuse = FUSE && fuse_count_;
+      // prefix pull + tail push on the first bottom-up level (see k_push_tail): both pulls use
+      // the 128-KB hub bitmap, whose range [0, H) is where the prefixes end
+      constexpr int kHubBig = 32768;
+      constexpr int32_t kPfxH = kHubBig * 32;
+      const bool pfx = pfx_ && first_bu && S.level == 2 && hub_lds && (hub_lds_ & 3) == 3 &&
+                       (hub_big_ & 3) == 3 && n > (int64_t)kHubBig * 32 * 4 && g_.rows_sorted &&
+                       n <= INT32_MAX;
+      if (pfx) {
+        ++epoch_;
+        k_push_tail<W><<<grid_for(S.nf, kBlock, 8192), kBlock, 0, s>>>(
+            fl_[S.fc].as<int32_t>(), S.nf, kPfxH, g_.rowptr, g_.col, R, codes, code_from,
+            done_.as<uint32_t>(), S.part, S.nparts, acc_[S.ac].as<uint64_t>(),
+            stamp_.as<int32_t>(), epoch_);
+        MSBFS_HIP_CHECK(hipGetLastError());
+      }
       if (S.nact) {
-        if (hub_lds && (hub_lds_ & 2)) {
+        if (pfx) {
+          constexpr int BT = 1024;
+          const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
+          auto kn = fuse ? k_bu_narrow<W, COUNT, BT, kHubBig, FUSE, true, true>
+                         : k_bu_narrow<W, COUNT, BT, kHubBig, false, true, true>;
+          kn<<<gn, BT, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
+                               sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
+                               fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+                               anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+                               next_wide, slabF(rows), acc_[S.ac].as<uint64_t>(),
+                               stamp_.as<int32_t>(), epoch_);
+          if (fuse) rows += gn;
+        } else if (hub_lds && (hub_lds_ & 2)) {
           constexpr int BT = 1024;
           const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
           // the narrow kernel runs one 1024-thread block per CU anyway (VGPR-bound), so its LDS
           // has room for a 4x larger hub bitmap (MSBFS_HUBBIG bit 0)
-          constexpr int kHubBig = 32768;  // 128 KB: ids < 1M
           const bool big = (hub_big_ & 1) && n > (int64_t)kHubBig * 32 * 4;
           auto kn = fuse ? (big ? k_bu_narrow<W, COUNT, BT, kHubBig, FUSE>
                                 : k_bu_narrow<W, COUNT, BT, kHubW, FUSE>)
@@ -2031,7 +2150,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                               next_wide, slabF(rows));
+                               next_wide, slabF(rows), nullptr, nullptr, 0);
           if (fuse) rows += gn;
         } else {
           const int gn = grid_for(S.nact, L::TILE, grid);
@@ -2045,21 +2164,32 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                    sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                    fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                    anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                                   next_wide, slabF(rows));
+                                   next_wide, slabF(rows), nullptr, nullptr, 0);
           if (fuse) rows += gn;
         }
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       if (S.nactw) {
-        frontier_degree_scan(g_.rowptr, actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(),
-                             scan_tmp_.p, scan_bytes_, s, kChunk);
+        if (pfx) {  // chunks of the row prefixes with ids < H only
+          int64_t* cnt = scan_tmp_.as<int64_t>();
+          char* t2 = (char*)scan_tmp_.p + (((size_t)S.nactw * sizeof(int64_t) + 255) & ~size_t(255));
+          const size_t tb = scan_bytes_ - (size_t)(t2 - (char*)scan_tmp_.p);
+          k_prefix_chunks<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
+              actw_[0].as<int32_t>(), S.nactw, g_.rowptr, g_.col, kPfxH, cnt);
+          MSBFS_HIP_CHECK(hipGetLastError());
+          inclusive_scan_i64(cnt, offs_.as<int64_t>(), S.nactw, t2, tb, s);
+        } else {
+          frontier_degree_scan(g_.rowptr, actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(),
+                               scan_tmp_.p, scan_bytes_, s, kChunk);
+        }
         const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
-        const bool use_xcd = first_bu && xcd_ && g_.rows_sorted && S.nactw >= 1024 && n <= INT32_MAX;
+        const bool use_xcd =
+            !pfx && first_bu && xcd_ && g_.rows_sorted && S.nactw >= 1024 && n <= INT32_MAX;
         if (!use_xcd) {
           desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
           k_chunk_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
-              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr,
-              desc_.as<ChunkDesc>());
+              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col,
+              pfx ? kPfxH : INT32_MAX, desc_.as<ChunkDesc>());
           MSBFS_HIP_CHECK(hipGetLastError());
         }
         if (use_xcd) {
@@ -2094,7 +2224,6 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         } else if (hub_lds && (hub_lds_ & 1)) {
           // exact chunk count = offs[nactw - 1], read on the device (no host round trip)
           // MSBFS_HUBBIG bit 1: one block per CU with a 128-KB hub bitmap (ids < 1M)
-          constexpr int kHubBig = 32768;
           const bool big = (hub_big_ & 2) && n > (int64_t)kHubBig * 32 * 4;
           auto ck = big ? k_bu_chunks<W, 256, 1024, kHubBig> : k_bu_chunks<W, 256, 1024, kHubW>;
           ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
