@@ -674,14 +674,18 @@ __global__ __launch_bounds__(kBlock) void k_push_tail(
     const int32_t* fl, int64_t nf, int32_t H, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, const uint16_t* code, int32_t code_from, const uint32_t* done,
     int part, int nparts, uint64_t* acc, int32_t* stamp, int32_t epoch) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nf;
-       i += (int64_t)gridDim.x * kBlock) {
-    const int32_t u = fl[i];
+  // one wave per frontier entry (tail vertices have up to a few hundred neighbours: the lanes
+  // take consecutive row entries)
+  const int lane = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t i = wave; i < nf; i += nwaves) {
+    const int32_t u = uni32(fl[i]);
     if (u < H) continue;
-    const uint32_t c = (code && u >= code_from) ? code[u] : kDenseCode;
+    const uint32_t c = (code && u >= code_from) ? (uint32_t)uni32(code[u]) : kDenseCode;
     if (c == 0) continue;
-    const int64_t b = rowptr[u], e = rowptr[u + 1];
-    for (int64_t k = b; k < e; ++k) {
+    const int64_t b = uni64(rowptr[u]), e = uni64(rowptr[u + 1]);
+    for (int64_t k = b + lane; k < e; k += 64) {
       const int32_t v = col[k];
       if (nparts > 1 && v % nparts != part) continue;
       if (is_done(done, v)) continue;
@@ -717,10 +721,9 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
-    int next_wide, uint32_t* slabF, uint64_t* pacc = nullptr, const int32_t* stamp = nullptr,
-    int32_t epoch = 0) {
+    int next_wide, uint32_t* slabF, uint64_t* pacc, const int32_t* stamp, int32_t epoch,
+    const int32_t* plen) {
   static_assert(!PFX || HUBW > 0, "the prefix pull relies on the LDS hub bitmap");
-  constexpr int32_t H = HUBW * 32;
   static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
@@ -760,21 +763,25 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
   uint32_t d1 = 0;
   if (tb + lofs < nact) v1 = act[tb + lofs];
   if (tb + stride + lofs < nact) v2 = act[tb + stride + lofs];
+  uint32_t p1 = 0;  // PFX: prefix length of v1's row (ids < H)
   if (tb + lofs < nact) {
     r1 = ldv<VW>(R + (int64_t)v1 * W + slot * VW);
     b1 = rowptr[v1];
     d1 = (uint32_t)(rowptr[v1 + 1] - b1);
+    if constexpr (PFX) p1 = (uint32_t)plen[v1];
   }
   int32_t u1[Q];  // first-step column ids of the current tile's vertex (third pipeline stage)
 #pragma unroll
   for (int q = 0; q < Q; ++q)
-    u1[q] = (tb + lofs < nact && (uint32_t)(q * G + slot) < d1) ? col[b1 + q * G + slot] : -1;
+    u1[q] = (tb + lofs < nact && (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
+                ? col[b1 + q * G + slot] : -1;
   for (; tb < nact; tb += stride) {
     const int64_t idx = tb + lofs;
     const bool valid = idx < nact;
     const int32_t v = valid ? v1 : 0;
     const V<VW> r = r1;
-    const int64_t beg = b1, end = b1 + d1;
+    const int64_t beg = b1, end = b1 + (PFX ? p1 : d1);  // PFX: pull only the prefix
+    const uint32_t deg = d1;
     int32_t u0[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) u0[q] = u1[q];
@@ -784,6 +791,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
       r1 = ldv<VW>(R + (int64_t)v1 * W + slot * VW);
       b1 = rowptr[v1];
       d1 = (uint32_t)(rowptr[v1 + 1] - b1);
+      if constexpr (PFX) p1 = (uint32_t)plen[v1];
     }
     if (idx + 2 * stride < nact) v2 = act[idx + 2 * stride];
     V<VW> unv = vzero<VW>(), acc = vzero<VW>();
@@ -811,15 +819,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
           const int64_t ee = e + q * G + slot;
           u[q] = e == beg ? u0[q] : (ee < end ? col[ee] : -1);  // first step: preloaded
         }
-        bool past = false;  // PFX: this step reached the row's ids >= H (sorted rows)
-        if constexpr (PFX) {
-#pragma unroll
-          for (int q = 0; q < Q; ++q)
-            if (u[q] >= H) {
-              u[q] = -1;
-              past = true;
-            }
-        }
+
         // ids below filter_from are loaded without a probe (filter off: filter_from = INT_MAX)
         // probes: every load first, every use after (with the use next to the load inside the
         // branch the compiler waited for each probe before issuing the next)
@@ -857,7 +857,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
         }
         // the whole group runs this loop in lock step (same v); exit when all lanes covered
         if (!((__ballot(!cov) >> (sub * G)) & L::GBITS)) break;
-        if (PFX && ((__ballot(past) >> (sub * G)) & L::GBITS)) break;
+
       }
     }
     V<VW> nw;
@@ -885,7 +885,6 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     const bool g_new = (bn >> (sub * G)) & L::GBITS;
     const bool g_nf = (bf >> (sub * G)) & L::GBITS;
     const bool leader = valid && slot == 0;
-    const uint32_t deg = (uint32_t)(end - beg);
     if (leader && !g_nf) set_done(done, v);
     const bool keep = leader && g_nf, app = leader && g_new;
     if (keep) eu += deg;
@@ -900,7 +899,8 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     // third stage: the next tile's first-step ids (its offsets arrived during this tile)
 #pragma unroll
     for (int q = 0; q < Q; ++q)
-      u1[q] = (idx + stride < nact && (uint32_t)(q * G + slot) < d1) ? col[b1 + q * G + slot] : -1;
+      u1[q] = (idx + stride < nact && (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
+                  ? col[b1 + q * G + slot] : -1;
     q_push(qa, keep && (int)deg <= next_wide, v);
     q_push(qw, keep && (int)deg > next_wide, v);
     q_push(qf, app, v);
@@ -1113,30 +1113,34 @@ __device__ __forceinline__ int64_t row_lower_bound(const int32_t* col, int64_t b
   return b;
 }
 
-// chunk counts of the wide vertices' row prefixes with ids < H (prefix-pull level, see
-// k_push_tail); inclusive-scanned into offs by the host
-__global__ __launch_bounds__(kBlock) void k_prefix_chunks(const int32_t* wl, int64_t nw,
-                                                          const int64_t* rowptr, const int32_t* col,
-                                                          int32_t H, int64_t* cnt) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
-       i += (int64_t)gridDim.x * kBlock) {
-    const int32_t v = wl[i];
+// plen[v] = length of v's row prefix with ids < H (rows sorted; a graph property, computed once
+// per graph and bound H, see BitparSolver::prefix_lens)
+__global__ __launch_bounds__(kBlock) void k_prefix_lens(const int64_t* rowptr, const int32_t* col,
+                                                        int64_t n, int32_t H, int32_t* plen) {
+  for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n;
+       v += (int64_t)gridDim.x * kBlock) {
     const int64_t b = rowptr[v];
-    cnt[i] = (row_lower_bound(col, b, rowptr[v + 1], H) - b + kChunk - 1) / kChunk;
+    plen[v] = (int32_t)(row_lower_bound(col, b, rowptr[v + 1], H) - b);
   }
 }
 
-// H < INT32_MAX: chunks cover only the row prefix with ids < H (rows sorted)
+// chunk counts of the wide vertices' row prefixes (inclusive-scanned into offs by the host)
+__global__ __launch_bounds__(kBlock) void k_prefix_chunks(const int32_t* wl, int64_t nw,
+                                                          const int32_t* plen, int64_t* cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
+       i += (int64_t)gridDim.x * kBlock)
+    cnt[i] = ((int64_t)plen[wl[i]] + kChunk - 1) / kChunk;
+}
+
+// plen != nullptr: chunks cover only the row prefixes with ids < H (prefix-pull level)
 __global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl, int64_t nw,
                                                        const int64_t* offs, const int64_t* rowptr,
-                                                       const int32_t* col, int32_t H,
-                                                       ChunkDesc* desc) {
+                                                       const int32_t* plen, ChunkDesc* desc) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
        i += (int64_t)gridDim.x * kBlock) {
     const int32_t v = wl[i];
     const int64_t b = rowptr[v];
-    int64_t e = rowptr[v + 1];
-    if (H != INT32_MAX) e = row_lower_bound(col, b, e, H);
+    const int64_t e = plen ? b + plen[v] : rowptr[v + 1];
     const int64_t c0 = i ? offs[i - 1] : 0, c1 = offs[i];
     for (int64_t c = c0; c < c1; ++c) {
       const int64_t cb = b + (c - c0) * kChunk;
@@ -1818,6 +1822,21 @@ class BitparSolver final : public Solver {
     return n_eff_;
   }
 
+  // plen[v] = row prefix length with ids < H for every vertex (cached per graph buffers and H)
+  const int32_t* prefix_lens(int32_t H, hipStream_t s) {
+    if (plen_key_[0] != (const void*)g_.rowptr || plen_key_[1] != (const void*)g_.col ||
+        plen_h_ != H) {
+      plen_.ensure((size_t)std::max<int64_t>(g_.n, 1) * sizeof(int32_t));
+      k_prefix_lens<<<grid_for(g_.n, kBlock, 8192), kBlock, 0, s>>>(g_.rowptr, g_.col, g_.n, H,
+                                                                     plen_.as<int32_t>());
+      MSBFS_HIP_CHECK(hipGetLastError());
+      plen_key_[0] = g_.rowptr;
+      plen_key_[1] = g_.col;
+      plen_h_ = H;
+    }
+    return plen_.as<int32_t>();
+  }
+
   HostCtr read_ctr(hipStream_t s) {
     MSBFS_HIP_CHECK(hipMemcpyAsync(hctr_->p, ctr_.p, sizeof(Ctr), hipMemcpyDeviceToHost, s));
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
@@ -1859,6 +1878,9 @@ class BitparSolver final : public Solver {
   // sparse row codes on the first bottom-up level (MSBFS_CODES=0: off); ids with degree >=
   // code_deg_ * nnz / (source degree sum), i.e. expected >= code_deg_ set bits, keep row gathers
   int codes_ = 1;
+  DevBuf plen_;
+  const void* plen_key_[2] = {nullptr, nullptr};
+  int32_t plen_h_ = 0;
   int pfx_ = 1;      // MSBFS_PFX=0: first bottom-up level pulls whole rows (no tail push)
   int hub_big_ = 3;  // MSBFS_HUBBIG: bit 0 narrow, bit 1 chunks use a 128-KB LDS hub bitmap
   double code_deg_ = 2.0;
@@ -2115,9 +2137,10 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       const bool pfx = pfx_ && first_bu && S.level == 2 && hub_lds && (hub_lds_ & 3) == 3 &&
                        (hub_big_ & 3) == 3 && n > (int64_t)kHubBig * 32 * 4 && g_.rows_sorted &&
                        n <= INT32_MAX;
+      const int32_t* plen = pfx ? prefix_lens(kPfxH, s) : nullptr;
       if (pfx) {
         ++epoch_;
-        k_push_tail<W><<<grid_for(S.nf, kBlock, 8192), kBlock, 0, s>>>(
+        k_push_tail<W><<<grid_for(S.nf * 64, kBlock, 8192), kBlock, 0, s>>>(
             fl_[S.fc].as<int32_t>(), S.nf, kPfxH, g_.rowptr, g_.col, R, codes, code_from,
             done_.as<uint32_t>(), S.part, S.nparts, acc_[S.ac].as<uint64_t>(),
             stamp_.as<int32_t>(), epoch_);
@@ -2134,7 +2157,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
                                next_wide, slabF(rows), acc_[S.ac].as<uint64_t>(),
-                               stamp_.as<int32_t>(), epoch_);
+                               stamp_.as<int32_t>(), epoch_, plen);
           if (fuse) rows += gn;
         } else if (hub_lds && (hub_lds_ & 2)) {
           constexpr int BT = 1024;
@@ -2150,7 +2173,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                               next_wide, slabF(rows), nullptr, nullptr, 0);
+                               next_wide, slabF(rows), nullptr, nullptr, 0, nullptr);
           if (fuse) rows += gn;
         } else {
           const int gn = grid_for(S.nact, L::TILE, grid);
@@ -2164,7 +2187,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                    sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                    fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                    anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                                   next_wide, slabF(rows), nullptr, nullptr, 0);
+                                   next_wide, slabF(rows), nullptr, nullptr, 0, nullptr);
           if (fuse) rows += gn;
         }
         MSBFS_HIP_CHECK(hipGetLastError());
@@ -2175,7 +2198,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           char* t2 = (char*)scan_tmp_.p + (((size_t)S.nactw * sizeof(int64_t) + 255) & ~size_t(255));
           const size_t tb = scan_bytes_ - (size_t)(t2 - (char*)scan_tmp_.p);
           k_prefix_chunks<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
-              actw_[0].as<int32_t>(), S.nactw, g_.rowptr, g_.col, kPfxH, cnt);
+              actw_[0].as<int32_t>(), S.nactw, plen, cnt);
           MSBFS_HIP_CHECK(hipGetLastError());
           inclusive_scan_i64(cnt, offs_.as<int64_t>(), S.nactw, t2, tb, s);
         } else {
@@ -2188,8 +2211,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         if (!use_xcd) {
           desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
           k_chunk_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
-              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, g_.col,
-              pfx ? kPfxH : INT32_MAX, desc_.as<ChunkDesc>());
+              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, plen,
+              desc_.as<ChunkDesc>());
           MSBFS_HIP_CHECK(hipGetLastError());
         }
         if (use_xcd) {
