@@ -179,9 +179,9 @@ __device__ __forceinline__ void slab_store(Lds<W, COUNT>& s, uint32_t* slabF,
 // Register-resident bit-sliced (carry-save) counters: bit b of c[j][d] is bit d of the count of
 // group (slot*VW + j)*64 + b. Adding a 64-bit new-bits word costs 2*D branch-free ops, vs one
 // LDS atomic per set bit in a divergent loop. Spilled to LDS every < 2^D additions.
-template <int VW>
+template <int VW, int DD = 6>
 struct BitCounter {
-  static constexpr int D = 6;
+  static constexpr int D = DD;
   uint64_t c[VW][D];
   __device__ __forceinline__ void zero() {
 #pragma unroll
@@ -749,7 +749,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long eu = 0, ef = 0, ev = 0;
-  BitCounter<VW> bc;
+  BitCounter<VW, PFX ? 5 : 6> bc;
   int nadd = 0;
   if constexpr (FUSE) bc.zero();
   // Software pipeline over the grid-stride tiles: the active-list entry is loaded two tiles
@@ -876,7 +876,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     }
     if constexpr (FUSE) {  // nw is zero for invalid lanes
       bc.add(nw);
-      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+      if (++nadd == (1 << BitCounter<VW, PFX ? 5 : 6>::D) - 1) {
         bc.spill(cnt, slot);
         nadd = 0;
       }
