@@ -1641,6 +1641,7 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
     if (const char* x = getenv("MSBFS_HUBBIG")) hub_big_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX")) pfx_ = atoi(x);
+    if (const char* x = getenv("MSBFS_PFX_H")) pfx_h_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
     bctr_.alloc((size_t)(kBatch + 1) * (sizeof(Ctr) + 16 * sizeof(uint64_t)));
@@ -1881,7 +1882,11 @@ class BitparSolver final : public Solver {
   DevBuf plen_;
   const void* plen_key_[2] = {nullptr, nullptr};
   int32_t plen_h_ = 0;
-  int pfx_ = 1;      // MSBFS_PFX=0: first bottom-up level pulls whole rows (no tail push)
+  // MSBFS_PFX: 0 = the first bottom-up level pulls whole rows (no tail push); 1 = prefix bound at
+  // the 128-KB hub bitmap (ids < 1M, one chunk block per CU); 2 (default) = at the 56-KB one
+  // (ids < 458752, two blocks per CU): RMAT-26 level 2 16.8 ms vs 18.1 (1) vs 21.2 (0)
+  int pfx_ = 2;
+  int32_t pfx_h_ = 0;  // MSBFS_PFX_H: lower prefix bound (tuning; smaller measured slower)
   int hub_big_ = 3;  // MSBFS_HUBBIG: bit 0 narrow, bit 1 chunks use a 128-KB LDS hub bitmap
   double code_deg_ = 2.0;
   std::map<int64_t, int32_t> code_bound_;
@@ -2133,10 +2138,14 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       // prefix pull + tail push on the first bottom-up level (see k_push_tail): both pulls use
       // the 128-KB hub bitmap, whose range [0, H) is where the prefixes end
       constexpr int kHubBig = 32768;
-      constexpr int32_t kPfxH = kHubBig * 32;
+      // MSBFS_PFX=2: prefix bound at the small hub bitmap (ids < 458752, two chunk blocks per CU,
+      // more tail pushes); 1: at the big one (ids < 1M)
+      const bool pfx_small = pfx_ == 2;
+      int32_t kPfxH = (pfx_small ? kHubW : kHubBig) * 32;
+      if (pfx_h_ > 0) kPfxH = std::min(kPfxH, pfx_h_);  // MSBFS_PFX_H: a lower bound (tuning)
       const bool pfx = pfx_ && first_bu && S.level == 2 && hub_lds && (hub_lds_ & 3) == 3 &&
-                       (hub_big_ & 3) == 3 && n > (int64_t)kHubBig * 32 * 4 && g_.rows_sorted &&
-                       n <= INT32_MAX;
+                       (pfx_small || (hub_big_ & 3) == 3) && n > (int64_t)kHubBig * 32 * 4 &&
+                       g_.rows_sorted && n <= INT32_MAX;
       const int32_t* plen = pfx ? prefix_lens(kPfxH, s) : nullptr;
       if (pfx) {
         ++epoch_;
@@ -2150,8 +2159,10 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         if (pfx) {
           constexpr int BT = 1024;
           const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
-          auto kn = fuse ? k_bu_narrow<W, COUNT, BT, kHubBig, FUSE, true, true>
-                         : k_bu_narrow<W, COUNT, BT, kHubBig, false, true, true>;
+          auto kn = fuse ? (pfx_small ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE, true, true>
+                                      : k_bu_narrow<W, COUNT, BT, kHubBig, FUSE, true, true>)
+                         : (pfx_small ? k_bu_narrow<W, COUNT, BT, kHubW, false, true, true>
+                                      : k_bu_narrow<W, COUNT, BT, kHubBig, false, true, true>);
           kn<<<gn, BT, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
                                sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
@@ -2247,7 +2258,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         } else if (hub_lds && (hub_lds_ & 1)) {
           // exact chunk count = offs[nactw - 1], read on the device (no host round trip)
           // MSBFS_HUBBIG bit 1: one block per CU with a 128-KB hub bitmap (ids < 1M)
-          const bool big = (hub_big_ & 2) && n > (int64_t)kHubBig * 32 * 4;
+          const bool big = (hub_big_ & 2) && n > (int64_t)kHubBig * 32 * 4 && !(pfx && pfx_small);
           auto ck = big ? k_bu_chunks<W, 256, 1024, kHubBig> : k_bu_chunks<W, 256, 1024, kHubW>;
           ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
               desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,

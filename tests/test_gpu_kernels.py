@@ -207,7 +207,7 @@ def test_bitpar_sparse_codes_relabelled(msbfs_pkg, K, monkeypatch):
 
 
 def test_bitpar_prefix_pull_tail_push(msbfs_pkg, monkeypatch):
-    """First bottom-up level as prefix pull (ids < 1M, LDS hub bitmap) + tail push (k_push_tail)
+    """First bottom-up level as prefix pull (ids below the LDS hub bound) + tail push (k_push_tail)
     on a relabelled RMAT-23 (n = 8M, large enough for the 128-KB hub bitmap): identical F with
     the prefix mode on and off, and equal to the per-group distance solver on a sample."""
     m = msbfs_pkg
@@ -215,13 +215,13 @@ def test_bitpar_prefix_pull_tail_push(msbfs_pkg, monkeypatch):
     g.relabel_by_degree()
     qs = m.QuerySet.random(g.n, 1024, 16, seed=11)
     out = {}
-    for pfx in ("1", "0"):
+    for pfx in ("2", "1", "0"):  # prefix bound 458752 / 1M / off
         monkeypatch.setenv("MSBFS_PFX", pfx)
         with m.Solver(g, "bitpar", max_groups=qs.K) as s:
             out[pfx] = s.run(qs).F
             tr = s.level_trace()
         assert tr[0]["dir"] == "T" and tr[1]["dir"] == "B"  # the prefix level is level 2
-    assert np.array_equal(out["1"], out["0"])
+    assert np.array_equal(out["1"], out["0"]) and np.array_equal(out["2"], out["0"])
     sub = qs.subset(np.arange(0, 1024, 128))
     with m.Solver(g, "dist") as ds:
         assert np.array_equal(ds.run(sub).F, out["1"][::128])

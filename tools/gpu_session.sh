@@ -92,6 +92,10 @@ for s in "$@"; do
     c26) for d in 1 4; do MSBFS_CODE_DEG=$d MSBFS_TRACE=1 step c26_$d 300 python bench.py --steps 2 --warmup 1; done ;;
     hubbig) for b in 1 2 3; do MSBFS_HUBBIG=$b MSBFS_TRACE=1 step hubbig$b 300 python bench.py --steps 2 --warmup 1; done
             MSBFS_HUBBIG=3 MSBFS_TRACE=1 step hubbig3g128 300 python bench.py --steps 2 --warmup 1 --groups 128 ;;
+    pfx2) MSBFS_PFX=2 MSBFS_TRACE=1 step pfx2_26 300 python bench.py --steps 2 --warmup 1 --verify 16
+          MSBFS_PFX=2 MSBFS_TRACE=1 step pfx2_128 300 python bench.py --steps 2 --warmup 1 --groups 128 ;;
+    pfxh) for h in 65536 131072 262144; do MSBFS_PFX=2 MSBFS_PFX_H=$h MSBFS_TRACE=1 step pfxh_$h 300 python bench.py --steps 2 --warmup 1
+          MSBFS_PFX=2 MSBFS_PFX_H=$h MSBFS_TRACE=1 step pfxh128_$h 300 python bench.py --steps 2 --warmup 1 --groups 128; done ;;
     hybsimall) step hybsimall 900 python tools/hybrid_sim.py --scale 26 --ranks 2 4 8 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
