@@ -312,7 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_
       if (!(old & bit)) {
         atomicOr((unsigned long long*)&visB[(int64_t)v * W + word], bit);
         atomicOr((unsigned long long*)&acc[(int64_t)v * W + word], bit);
-        atomicOr((unsigned long long*)&alive[word], bit);
+        (void)alive;  // alive (groups with a valid source) is uploaded by the host
         const unsigned long long deg = (unsigned long long)(rowptr[v + 1] - rowptr[v]);
         if constexpr (COUNT) atomicAdd(&E[k], deg);
         app = atomicExch(&stamp[v], epoch) != epoch;
@@ -674,18 +674,19 @@ __global__ __launch_bounds__(kBlock) void k_push_tail(
     const int32_t* fl, int64_t nf, int32_t H, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, const uint16_t* code, int32_t code_from, const uint32_t* done,
     int part, int nparts, uint64_t* acc, int32_t* stamp, int32_t epoch) {
-  // one wave per frontier entry (tail vertices have up to a few hundred neighbours: the lanes
-  // take consecutive row entries)
-  const int lane = lane_id();
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
-  for (int64_t i = wave; i < nf; i += nwaves) {
-    const int32_t u = uni32(fl[i]);
+  // 16 lanes per frontier entry, 4 entries per wave in flight (tail vertices have tens to a few
+  // hundred neighbours; the lanes of an entry take consecutive row entries)
+  constexpr int PG = 64;
+  const int lane = lane_id(), slot = lane % PG;
+  const int64_t grp = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / PG;
+  const int64_t ngrp = ((int64_t)gridDim.x * kBlock) / PG;
+  for (int64_t i = grp; i < nf; i += ngrp) {
+    const int32_t u = fl[i];
     if (u < H) continue;
-    const uint32_t c = (code && u >= code_from) ? (uint32_t)uni32(code[u]) : kDenseCode;
+    const uint32_t c = (code && u >= code_from) ? (uint32_t)code[u] : kDenseCode;
     if (c == 0) continue;
-    const int64_t b = uni64(rowptr[u]), e = uni64(rowptr[u + 1]);
-    for (int64_t k = b + lane; k < e; k += 64) {
+    const int64_t b = rowptr[u], e = rowptr[u + 1];
+    for (int64_t k = b + slot; k < e; k += PG) {
       const int32_t v = col[k];
       if (nparts > 1 && v % nparts != part) continue;
       if (is_done(done, v)) continue;
@@ -1936,12 +1937,6 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
   MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
   MSBFS_HIP_CHECK(hipMemsetAsync(small_.p, 0, small_.bytes, s));
   const Small sm = small();
-  {
-    uint64_t hm[16] = {0};
-    for (int64_t k = 0; k < nb; ++k) hm[k >> 6] |= 1ull << (k & 63);
-    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, hm, sizeof(hm), hipMemcpyHostToDevice, s));
-    MSBFS_HIP_CHECK(hipStreamSynchronize(s));  // hm is a stack buffer
-  }
   // ---- sources: (vertex, local group) pairs, out-of-range ids dropped (main.cu:49)
   std::vector<int32_t> hp, hk;
   hp.reserve(2 * (qoff[k0 + nb] - qoff[k0]));
@@ -1954,6 +1949,16 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
       }
     }
   const int64_t np = (int64_t)hp.size();
+  {
+    // gmask = the batch's groups; alive = groups with at least one valid source (computed here:
+    // an atomicOr per source pair onto 16 words serialised k_init, ~0.1 ms per batch)
+    uint64_t hm[2][16] = {{0}};
+    for (int64_t k = 0; k < nb; ++k) hm[0][k >> 6] |= 1ull << (k & 63);
+    for (int64_t i = 0; i < np; ++i) hm[1][hk[i] >> 6] |= 1ull << (hk[i] & 63);
+    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, hm[0], sizeof(hm[0]), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[0], hm[1], sizeof(hm[1]), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));  // hm is a stack buffer
+  }
   pairs_.ensure((size_t)std::max<int64_t>(np, 1) * 2 * sizeof(int32_t));
   int32_t* dpv = pairs_.as<int32_t>();
   int32_t* dpk = dpv + std::max<int64_t>(np, 1);
