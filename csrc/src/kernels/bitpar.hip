@@ -717,7 +717,11 @@ __global__ __launch_bounds__(kBlock) void k_push_tail(
 // separate k_count_frontier pass that re-reads both rows of every new frontier vertex.
 // PFX (prefix-pull level, see k_push_tail): rows are scanned only up to the first id >= HUBW*32,
 // and pushed bits (acc of vertices with stamp == epoch) seed the accumulator.
-template <int W, bool COUNT, int BT, int HUBW, bool FUSE, bool FILT = true, bool PFX = false>
+// CS = neighbours per step (rows gathered between two coverage checks).
+// C1 > 0 (unfiltered levels only): a first step of just C1 rows before the CS-wide steps; late
+// levels are mostly covered by the first neighbour or two (sorted rows: hubs first).
+template <int W, bool COUNT, int BT, int HUBW, bool FUSE, bool FILT = true, bool PFX = false,
+          int CS = 8, int C1 = 0>
 __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
@@ -729,9 +733,9 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
   constexpr int NWV = BT / 64, TILE = NWV * VPW;
-  constexpr int C = 8;                       // neighbours per step
+  constexpr int C = CS;                      // neighbours per step
   constexpr int Q = C / G > 0 ? C / G : 1;   // ids loaded per lane per step
-  static_assert(G * Q == C, "lane groups of 1..8 lanes");
+  static_assert(G * Q == C || (C < G && Q == 1), "step = whole lane groups or part of one");
   __shared__ LdsQueue qa, qf, qw;
   __shared__ unsigned long long scratch[NWV];
   __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
@@ -774,7 +778,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
   int32_t u1[Q];  // first-step column ids of the current tile's vertex (third pipeline stage)
 #pragma unroll
   for (int q = 0; q < Q; ++q)
-    u1[q] = (tb + lofs < nact && (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
+    u1[q] = (tb + lofs < nact && q * G + slot < C && (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
                 ? col[b1 + q * G + slot] : -1;
   for (; tb < nact; tb += stride) {
     const int64_t idx = tb + lofs;
@@ -812,13 +816,37 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
       }
     }
     const bool g_open = valid && ((__ballot(lane_open) >> (sub * G)) & L::GBITS);
-    if (g_open) {
-      for (int64_t e = beg; e < end; e += C) {
+    int64_t e0 = beg;
+    bool g_cov = false;
+    if constexpr (C1 > 0) {
+      static_assert(!FILT, "the short first step skips the filter");
+      if (g_open) {
+        V<VW> x[C1];
+#pragma unroll
+        for (int c = 0; c < C1; ++c) {
+          const int32_t uc = G == 1 ? u0[c] : __shfl(u0[c / G], sub * G + (c % G));
+          x[c] = uc >= 0 ? ldv<VW>(R + (int64_t)uc * W + slot * VW) : vzero<VW>();
+        }
+        bool cov = true;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+#pragma unroll
+          for (int c = 0; c < C1; ++c) acc.w[j] |= x[c].w[j];
+          cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
+        }
+        g_cov = !((__ballot(!cov) >> (sub * G)) & L::GBITS);
+        e0 = beg + C1;
+      }
+    }
+    if (g_open && !g_cov) {
+      for (int64_t e = e0; e < end; e += C) {
         int32_t u[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
           const int64_t ee = e + q * G + slot;
-          u[q] = e == beg ? u0[q] : (ee < end ? col[ee] : -1);  // first step: preloaded
+          // first step: preloaded (without the short first step)
+          u[q] = (C1 == 0 && e == beg) ? u0[q]
+                                       : ((q * G + slot < C && ee < end) ? col[ee] : -1);
         }
 
         // ids below filter_from are loaded without a probe (filter off: filter_from = INT_MAX)
@@ -900,7 +928,8 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     // third stage: the next tile's first-step ids (its offsets arrived during this tile)
 #pragma unroll
     for (int q = 0; q < Q; ++q)
-      u1[q] = (idx + stride < nact && (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
+      u1[q] = (idx + stride < nact && q * G + slot < C &&
+               (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
                   ? col[b1 + q * G + slot] : -1;
     q_push(qa, keep && (int)deg <= next_wide, v);
     q_push(qw, keep && (int)deg > next_wide, v);
@@ -1642,6 +1671,7 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
     if (const char* x = getenv("MSBFS_HUBBIG")) hub_big_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX")) pfx_ = atoi(x);
+    if (const char* x = getenv("MSBFS_NARROW_C")) narrow_c_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX_H")) pfx_h_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
@@ -1888,6 +1918,7 @@ class BitparSolver final : public Solver {
   // (ids < 458752, two blocks per CU): RMAT-26 level 2 16.8 ms vs 18.1 (1) vs 21.2 (0)
   int pfx_ = 2;
   int32_t pfx_h_ = 0;  // MSBFS_PFX_H: lower prefix bound (tuning; smaller measured slower)
+  int narrow_c_ = 2;   // MSBFS_NARROW_C: short first narrow step (0 off, 1 always, 2 by level)
   int hub_big_ = 3;  // MSBFS_HUBBIG: bit 0 narrow, bit 1 chunks use a 128-KB LDS hub bitmap
   double code_deg_ = 2.0;
   std::map<int64_t, int32_t> code_bound_;
@@ -2195,8 +2226,14 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           const int gn = grid_for(S.nact, L::TILE, grid);
           // FILT = false: no probe code at all (fewer VGPRs) on the levels that load every row
           const bool filt = filter_from != INT32_MAX;
+          // short first step (one row) from the third bottom-up level on, or with few words: by
+          // then most vertices are covered by their first neighbour (RMAT-26, 1024 groups: level
+          // 4 3.1 -> 2.5 ms; level 3 prefers full steps: 6.5 vs 6.7 ms). MSBFS_NARROW_C: 0 off,
+          // 1 always, 2 (default) this rule
+          const bool short1 = narrow_c_ == 1 || (narrow_c_ == 2 && (S.bu_levels >= 3 || W <= 4));
           auto kn = fuse ? (filt ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, true>
-                                 : k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false>)
+                                 : short1 ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1>
+                                          : k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false>)
                          : (filt ? k_bu_narrow<W, COUNT, kBlock, 0, false, true>
                                  : k_bu_narrow<W, COUNT, kBlock, 0, false, false>);
           kn<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
