@@ -125,3 +125,22 @@ def test_cli_fault_takes_job_down(tmp_path, msbfs_pkg, fault):
     assert r.returncode != 0
     err = (tmp_path / f"err.{rank}").read_text()
     assert f"injected fault: {fault.split(':')[0]} on rank {rank}" in err
+
+
+def test_cli_baseline_config1_serial_cpu(msbfs_pkg):
+    """BASELINE config 1: 1K-vertex / 10K-edge random graph, 4 single-source queries, serial CPU
+    BFS on one rank (plumbing, no GPU) — checked against the numpy oracle of the reference
+    semantics (ops/reference.py)."""
+    m = msbfs_pkg
+    r = _run([_cli(m), "--gen", "uniform:1000:10000:1", "--qgen", "4:1:7", "-gn", "1", "--algo",
+              "cpu", "--threads", "1", "--json"], {"MSBFS_NO_MPI": "1"})
+    assert r.returncode == 0, r.stderr
+    g = m.Graph.uniform(1000, 10000, 1)
+    qs = m.QuerySet.random(g.n, 4, 1, 7)
+    from msbfs.ops.reference import bfs_F_numpy
+    F = [bfs_F_numpy(g.n, g.rowptr, g.col, qs.group(k))[0] for k in range(qs.K)]
+    import json
+    js = json.loads(r.stdout.splitlines()[7])
+    assert js["F"] == F and js["K"] == 4 and js["n"] == 1000
+    k = int(np.argmin(F))
+    assert r.stdout.splitlines()[2] == f"Query number (k) with minimum F value: {k + 1}"
