@@ -110,18 +110,23 @@ def main() -> int:
     # untimed: every candidate decomposition once (correctness check against the round-robin
     # pass via the gathered F vector, and its time, max over ranks); the fastest one is timed
     F_ref = D.gather_F(r0.F, rr_idx, qs.K, ctx)
+    # Each candidate runs twice and keeps its faster time: the first run of a decomposition can
+    # carry one-time costs (e.g. RCCL setting up the all-to-all's peer connections) that would
+    # otherwise decide the choice.
     cand_ms = {}
     for m in candidates:
-        D.barrier(ctx)
-        torch.cuda.synchronize(dev)
-        t = time.perf_counter()
-        Fm, _ = step(m)
-        torch.cuda.synchronize(dev)
-        cand_ms[m] = D.allreduce_max(time.perf_counter() - t, ctx) * 1e3
-        Fg = D.gather_F(Fm, plans[m][1], qs.K, ctx)  # identical on every rank
-        if not np.array_equal(Fg, F_ref):
-            print(f"rank {ctx.rank}: {m} F differs from the round-robin pass", file=sys.stderr)
-            return 3
+        for rep in range(2 if ctx.world > 1 else 1):
+            D.barrier(ctx)
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            Fm, _ = step(m)
+            torch.cuda.synchronize(dev)
+            ms = D.allreduce_max(time.perf_counter() - t, ctx) * 1e3
+            cand_ms[m] = min(cand_ms.get(m, ms), ms)
+            Fg = D.gather_F(Fm, plans[m][1], qs.K, ctx)  # identical on every rank
+            if not np.array_equal(Fg, F_ref):
+                print(f"rank {ctx.rank}: {m} F differs from the round-robin pass", file=sys.stderr)
+                return 3
     mode = min(cand_ms, key=cand_ms.get)
     local_idx = plans[mode][1]
     if args.verify and ctx.rank == 0:
