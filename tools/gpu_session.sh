@@ -98,6 +98,7 @@ for s in "$@"; do
           MSBFS_PFX=2 MSBFS_PFX_H=$h MSBFS_TRACE=1 step pfxh128_$h 300 python bench.py --steps 2 --warmup 1 --groups 128; done ;;
     narrowc) for c in 1 2; do MSBFS_NARROW_C=$c MSBFS_TRACE=1 step nc$c 300 python bench.py --steps 2 --warmup 1 --verify 16
             MSBFS_NARROW_C=$c MSBFS_TRACE=1 step nc128_$c 300 python bench.py --steps 2 --warmup 1 --groups 128; done ;;
+    hyb2trace) MSBFS_TRACE=1 step hyb2trace 600 python tools/hybrid_sim.py --scale 26 --ranks 2 --no-roundrobin ;;
     hybsimall) step hybsimall 900 python tools/hybrid_sim.py --scale 26 --ranks 2 4 8 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
