@@ -11,6 +11,9 @@ step() {
   local rc=$?
   echo "== $name rc=$rc"; tail -n 5 "gpurun_out/$name.log"
   if [ $rc -gt 1 ]; then echo "stopping: $name exited $rc"; exit $rc; fi
+  # a GPU fault inside a Python process surfaces as an exception (status 1): stop there too
+  if grep -qE "illegal memory access|Memory access fault|hipErrorLaunchFailure|HSA_STATUS_ERROR" \
+      "gpurun_out/$name.log"; then echo "stopping: GPU fault in $name"; exit 3; fi
   return 0
 }
 for s in "$@"; do
