@@ -82,6 +82,13 @@ struct DeviceGraph {
   // every row's neighbour ids ascending (device_graph_sort_rows; relabelling sorts too). Solvers
   // may binary-search rows only when this is set.
   bool rows_sorted = false;
+  // How a device-generated graph was made (0 = not generated, 1 = RMAT, 2 = uniform): a
+  // relabelling that has no room for a second column array regenerates the edges straight into
+  // the new ids instead (the generators are deterministic functions of the edge index).
+  int gen_kind = 0;
+  RmatParams gen_rmat{};
+  uint64_t gen_seed = 0;
+  int64_t gen_edges = 0;
 };
 
 // Stats returned by solvers (mirrors msbfs_stats in msbfs.h). recs: one record per BFS level

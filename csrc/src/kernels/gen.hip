@@ -14,13 +14,18 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// map != nullptr: endpoints are renumbered through it (relabelled regeneration)
 __global__ __launch_bounds__(kBlock) void k_rmat_pass(RmatParams p, int64_t m,
                                                       unsigned long long* cnt, int32_t* col,
-                                                      int scatter) {
+                                                      int scatter, const int32_t* map = nullptr) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
     uint32_t u, v;
     rmat_edge(p, (uint64_t)i, u, v);
+    if (map) {
+      u = (uint32_t)map[u];
+      v = (uint32_t)map[v];
+    }
     if (!scatter) {
       atomicAdd(&cnt[u], 1ull);
       atomicAdd(&cnt[v], 1ull);
@@ -33,11 +38,15 @@ __global__ __launch_bounds__(kBlock) void k_rmat_pass(RmatParams p, int64_t m,
 
 __global__ __launch_bounds__(kBlock) void k_uniform_pass(uint64_t seed, int64_t n, int64_t m,
                                                          unsigned long long* cnt, int32_t* col,
-                                                         int scatter) {
+                                                         int scatter, const int32_t* map = nullptr) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
     uint32_t u, v;
     uniform_edge(seed, (uint64_t)i, (uint64_t)n, u, v);
+    if (map) {
+      u = (uint32_t)map[u];
+      v = (uint32_t)map[v];
+    }
     if (!scatter) {
       atomicAdd(&cnt[u], 1ull);
       atomicAdd(&cnt[v], 1ull);
@@ -255,6 +264,9 @@ void device_graph_gen_rmat(DeviceGraph& g, int scale, int64_t edgefactor, uint64
   build_from_counts(g, cnt, s);
   k_rmat_pass<<<grid, kBlock, 0, s>>>(p, m, cnt.as<unsigned long long>(), g.col, 1);
   MSBFS_HIP_CHECK(hipGetLastError());
+  g.gen_kind = 1;
+  g.gen_rmat = p;
+  g.gen_edges = m;
   device_graph_stats(g, s);
 }
 
@@ -273,6 +285,9 @@ void device_graph_gen_uniform(DeviceGraph& g, int64_t n, int64_t m, uint64_t see
     k_uniform_pass<<<grid, kBlock, 0, s>>>(seed, n, m, cnt.as<unsigned long long>(), g.col, 1);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
+  g.gen_kind = 2;
+  g.gen_seed = seed;
+  g.gen_edges = m;
   device_graph_stats(g, s);
 }
 
@@ -313,11 +328,17 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(const int64_t* orow, con
 void device_graph_relabel_by_degree(DeviceGraph& g, hipStream_t s) {
   const int64_t n = g.n;
   if (n == 0 || g.old2new) return;
+  // The rebuild holds a second column array next to the first. A device-generated graph without
+  // room for it (RMAT-30: 128 GiB of columns) is regenerated in the new ids instead: same rows,
+  // and after the row sort the same CSR. MSBFS_RELABEL_REGEN=1 forces that path (tests).
+  bool regen = false;
   {
-    // the rebuild holds a second column array next to the first
     size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
-        (double)free_b < 1.05 * ((double)g.nnz * 4.0 + (double)n * 40.0))
+    const bool tight = hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+                       (double)free_b < 1.05 * ((double)g.nnz * 4.0 + (double)n * 40.0);
+    const char* force = getenv("MSBFS_RELABEL_REGEN");
+    regen = g.gen_kind != 0 && (tight || (force && atoi(force) != 0));
+    if (tight && !regen)
       fail("not enough device memory to relabel the graph (needs a second " +
            std::to_string(g.nnz * 4 >> 20) + " MiB column array)");
   }
@@ -355,11 +376,34 @@ void device_graph_relabel_by_degree(DeviceGraph& g, hipStream_t s) {
                                                      nrow.as<int64_t>() + 1, (int)n, s));
   }
   newdeg.release();
-  DevBuf ncol((size_t)std::max<int64_t>(g.nnz, 1) * 4);
-  k_gather_rows<<<grid_for(n * 64, kBlock, 8192), kBlock, 0, s>>>(
-      g.rowptr, g.col, perm.as<int32_t>(), nrow.as<int64_t>(), o2n, ncol.as<int32_t>(), n);
-  MSBFS_HIP_CHECK(hipGetLastError());
-  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  DevBuf ncol;
+  if (regen) {
+    // scatter the regenerated edges into the new rows (cursor = new row starts)
+    perm.release();
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    g.own_col.release();
+    g.col = nullptr;
+    ncol.alloc((size_t)std::max<int64_t>(g.nnz, 1) * 4);
+    DevBuf cur((size_t)n * sizeof(int64_t));
+    k_copy_i64<<<grid_for(n, kBlock), kBlock, 0, s>>>(nrow.as<int64_t>(), cur.as<int64_t>(), n);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    const int64_t m = g.gen_edges;
+    const int grid = grid_for(m, kBlock, 8192);
+    if (m && g.gen_kind == 1)
+      k_rmat_pass<<<grid, kBlock, 0, s>>>(g.gen_rmat, m, cur.as<unsigned long long>(),
+                                          ncol.as<int32_t>(), 1, o2n);
+    else if (m)
+      k_uniform_pass<<<grid, kBlock, 0, s>>>(g.gen_seed, n, m, cur.as<unsigned long long>(),
+                                             ncol.as<int32_t>(), 1, o2n);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  } else {
+    ncol.alloc((size_t)std::max<int64_t>(g.nnz, 1) * 4);
+    k_gather_rows<<<grid_for(n * 64, kBlock, 8192), kBlock, 0, s>>>(
+        g.rowptr, g.col, perm.as<int32_t>(), nrow.as<int64_t>(), o2n, ncol.as<int32_t>(), n);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  }
   g.own_rowptr = std::move(nrow);
   g.own_col = std::move(ncol);
   g.rowptr = g.own_rowptr.as<int64_t>();

@@ -168,6 +168,26 @@ def test_relabelled_graph_same_answers(msbfs_pkg, algo):
     assert np.array_equal(res.edges, ref.edges)
 
 
+@pytest.mark.parametrize("kind", ["rmat", "uniform"])
+def test_relabel_by_regeneration_matches(msbfs_pkg, kind, monkeypatch):
+    """The low-memory relabel path (device-generated graphs are regenerated straight into the
+    new ids when a second column array does not fit, e.g. RMAT-30) gives the same CSR and map as
+    the gather path."""
+    m = msbfs_pkg
+    make = ((lambda: m.DeviceGraph.rmat(15, 16, 9, device=0)) if kind == "rmat"
+            else (lambda: m.DeviceGraph.uniform(30000, 250000, 4, device=0)))
+    monkeypatch.delenv("MSBFS_RELABEL_REGEN", raising=False)
+    a = make()
+    a.relabel_by_degree()
+    monkeypatch.setenv("MSBFS_RELABEL_REGEN", "1")
+    b = make()
+    b.relabel_by_degree()
+    ga, gb = a.download(), b.download()
+    assert np.array_equal(a.relabel_map(), b.relabel_map())
+    assert np.array_equal(ga.rowptr, gb.rowptr)
+    assert np.array_equal(ga.col, gb.col)
+
+
 def test_bitpar_level_trace(msbfs_pkg):
     """Per-level records (msbfs_solver_levels): one per level, consistent with the stats and with
     the frontier chain (the next level starts from the previous level's new vertices)."""

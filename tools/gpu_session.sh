@@ -103,6 +103,10 @@ for s in "$@"; do
             MSBFS_NARROW_C=$c MSBFS_TRACE=1 step nc128_$c 300 python bench.py --steps 2 --warmup 1 --groups 128; done ;;
     hyb2trace) MSBFS_TRACE=1 step hyb2trace 600 python tools/hybrid_sim.py --scale 26 --ranks 2 --no-roundrobin ;;
     hybsimall) step hybsimall 900 python tools/hybrid_sim.py --scale 26 --ranks 2 4 8 ;;
+    hybpfx) for x in 2 0 1; do MSBFS_PFX=$x step hybpfx_$x 600 python tools/hybrid_sim.py --scale 26 --ranks 4 8 --no-roundrobin; done ;;
+    regen) step regen 300 python -m pytest tests/test_gpu_kernels.py -m gpu -x -q -k "regeneration or relabelled" ;;
+    rmat30) MSBFS_TRACE=1 step rmat30 1000 python bench.py --scale 30 --groups 256 --steps 1 --warmup 0 ;;
+    prof30) export TMPDIR=/tmp; rm -rf gpurun_out/prof30; step prof30 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof30 -o run -- python bench.py --scale 30 --groups 256 --steps 1 --warmup 0 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
