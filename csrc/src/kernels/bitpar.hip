@@ -1699,6 +1699,8 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_HUBBIG")) hub_big_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX")) pfx_ = atoi(x);
     if (const char* x = getenv("MSBFS_NARROW_C")) narrow_c_ = atoi(x);
+    if (const char* x = getenv("MSBFS_COOP")) coop_ = atoi(x);
+    if (const char* x = getenv("MSBFS_GAMMA")) gamma_ = atof(x);
     if (const char* x = getenv("MSBFS_PFX_H")) pfx_h_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
@@ -1945,6 +1947,8 @@ class BitparSolver final : public Solver {
   // (ids < 458752, two blocks per CU): RMAT-26 level 2 16.8 ms vs 18.1 (1) vs 21.2 (0)
   int pfx_ = 2;
   int32_t pfx_h_ = 0;  // MSBFS_PFX_H: lower prefix bound (tuning; smaller measured slower)
+  double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
+  int coop_ = -1;      // MSBFS_COOP: cross-chunk early exit on the first pull level (-1 auto)
   int narrow_c_ = 2;   // MSBFS_NARROW_C: short first narrow step (0 off, 1 always, 2 by level)
   int hub_big_ = 3;  // MSBFS_HUBBIG: bit 0 narrow, bit 1 chunks use a 128-KB LDS hub bitmap
   double code_deg_ = 2.0;
@@ -2060,7 +2064,14 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
     bool& bottom_up = S.bottom_up;
     if (opt.force_dir == 1) bottom_up = false;
     else if (opt.force_dir == 2) bottom_up = S.level > 0;
-    else if (!bottom_up) bottom_up = (double)S.ef > (double)S.ea / opt.alpha;
+    else if (!bottom_up)
+      // Beamer's edge test, plus a vertex test: a pull level costs about one visit per
+      // non-isolated vertex (prefix pulls, early exit), a push level one scattered atomic per
+      // frontier edge, so pull once the frontier has more edges than the graph has vertices
+      // (RMAT-30, 256 groups: 742 -> 294 ms/step; RMAT-26, 16 groups: 16.4 -> 9.3 ms; road
+      // graphs never get there). MSBFS_GAMMA scales the vertex test (0 turns it off).
+      bottom_up = (double)S.ef > (double)S.ea / opt.alpha ||
+                  (gamma_ > 0 && S.level >= 1 && (double)S.ef > gamma_ * (double)n_eff());
     else bottom_up = !((double)S.nf < (double)S.na / opt.beta && (double)S.ef < (double)S.ea / opt.alpha);
     if (S.level < dirs_.size() && (dirs_[S.level] == 'T' || dirs_[S.level] == 'B'))
       bottom_up = dirs_[S.level] == 'B';
@@ -2286,6 +2297,12 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                scan_tmp_.p, scan_bytes_, s, kChunk);
         }
         const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
+        // Early exit across a vertex's chunks (coop) everywhere except on an explosive first
+        // bottom-up level (level 2: hardly any row gets covered, and round-robin chunk dealing
+        // balances the hubs better). When top-down ran longer (RMAT-30: first pull at level 3,
+        // most of every hub's groups already visited) the early exit skips most chunks.
+        // MSBFS_COOP: 1 always, 0 = never on the first bottom-up level (the old rule).
+        const int coop = !first_bu ? 1 : coop_ == 1 ? 1 : coop_ == 0 ? 0 : (S.level == 2 ? 0 : 1);
         const bool use_xcd =
             !pfx && first_bu && xcd_ && g_.rows_sorted && S.nactw >= 1024 && n <= INT32_MAX;
         if (!use_xcd) {
@@ -2332,13 +2349,13 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
               desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
               sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-              first_bu ? 0 : 1, xmode_, codes, code_from);
+              coop, xmode_, codes, code_from);
         } else {
           auto ck = tile_ >= 1024 ? k_bu_chunks<W, 1024, kBlock, 0>
                     : tile_ >= 512 ? k_bu_chunks<W, 512, kBlock, 0> : k_bu_chunks<W, 256, kBlock, 0>;
           ck<<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
               desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(),
-              anyvis_.as<uint32_t>(), filter_from, first_bu ? 0 : 1, xmode_, codes, code_from);
+              anyvis_.as<uint32_t>(), filter_from, coop, xmode_, codes, code_from);
         }
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(S.nactw, L::TILE, grid);

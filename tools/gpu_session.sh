@@ -106,7 +106,23 @@ for s in "$@"; do
     hybpfx) for x in 2 0 1; do MSBFS_PFX=$x step hybpfx_$x 600 python tools/hybrid_sim.py --scale 26 --ranks 4 8 --no-roundrobin; done ;;
     regen) step regen 300 python -m pytest tests/test_gpu_kernels.py -m gpu -x -q -k "regeneration or relabelled" ;;
     rmat30) MSBFS_TRACE=1 step rmat30 1000 python bench.py --scale 30 --groups 256 --steps 1 --warmup 0 ;;
-    prof30) export TMPDIR=/tmp; rm -rf gpurun_out/prof30; step prof30 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof30 -o run -- python bench.py --scale 30 --groups 256 --steps 1 --warmup 0 ;;
+    prof30) export TMPDIR=/tmp; rm -rf gpurun_out/prof30; step prof30 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof30 -o run -- python bench.py --scale 30 --groups 256 --steps 1 --warmup 0 &&
+            python tools/prof_summary.py gpurun_out/prof30 > gpurun_out/prof30.md && rm -f gpurun_out/prof30/run_kernel_trace.csv ;;
+    r30coop) for x in -1 0; do MSBFS_COOP=$x MSBFS_TRACE=1 step r30coop_$x 600 python bench.py --scale 30 --groups 256 --steps 1 --warmup 0; done &&
+             MSBFS_DIRS=TBBBBBBBBBBBBBBBBBBB MSBFS_TRACE=1 step r30tb 600 python bench.py --scale 30 --groups 256 --steps 1 --warmup 0 ;;
+    alpha) for a in 14 32 64; do
+             step al22_$a 300 python bench.py --scale 22 --groups 64 --steps 5 --warmup 1 --alpha $a &&
+             step al26g16_$a 300 python bench.py --groups 16 --steps 3 --warmup 1 --alpha $a &&
+             step al26g128_$a 300 python bench.py --groups 128 --steps 3 --warmup 1 --alpha $a &&
+             step al26_$a 300 python bench.py --steps 3 --warmup 1 --alpha $a &&
+             step al30_$a 600 python bench.py --scale 30 --groups 256 --steps 1 --warmup 0 --alpha $a &&
+             step alroad_$a 600 python tools/bench_graph.py --graph grid:4896:4896:0.6 --groups 64 --steps 1 --alpha $a || exit 1; done ;;
+    dirchk) step dc22 300 python bench.py --scale 22 --groups 64 --steps 5 --warmup 1 --verify 16 &&
+            step dc26g16 300 python bench.py --groups 16 --steps 3 --warmup 1 --verify 4 &&
+            step dc26g128 300 python bench.py --groups 128 --steps 3 --warmup 1 &&
+            step dc26 300 python bench.py --steps 3 --warmup 1 &&
+            step dc30 600 python bench.py --scale 30 --groups 256 --steps 2 --warmup 1 &&
+            step dcroad 600 python tools/bench_graph.py --graph grid:4896:4896:0.6 --groups 64 --steps 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
