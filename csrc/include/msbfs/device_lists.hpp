@@ -13,19 +13,25 @@ namespace msbfs {
 
 constexpr int kQCap = 1024;  // LDS queue capacity (items) per block
 
-struct LdsQueue {
-  int32_t item[kQCap];
+// CAP items; bigger queues (full-graph list builds) mean fewer flushes, i.e. fewer atomics on
+// the one global counter, which the memory side executes one at a time
+template <int CAP>
+struct LdsQueueN {
+  int32_t item[CAP];
   uint32_t n;
   uint32_t base;
 };
+using LdsQueue = LdsQueueN<kQCap>;
 
 // Call from every thread, followed by a __syncthreads() before the first push.
-__device__ __forceinline__ void q_init(LdsQueue& q) {
+template <int CAP>
+__device__ __forceinline__ void q_init(LdsQueueN<CAP>& q) {
   if (threadIdx.x == 0) q.n = 0;
 }
 
 // wave-aggregated push into the block queue (call from converged wave code)
-__device__ __forceinline__ void q_push(LdsQueue& q, bool pred, int32_t v) {
+template <int CAP>
+__device__ __forceinline__ void q_push(LdsQueueN<CAP>& q, bool pred, int32_t v) {
   const uint64_t mask = __ballot(pred);
   if (!mask) return;
   const int leader = __ffsll((unsigned long long)mask) - 1;
@@ -37,12 +43,13 @@ __device__ __forceinline__ void q_push(LdsQueue& q, bool pred, int32_t v) {
 
 // Flush the queue to out[] when it may not hold another `room` items (or always, at the end).
 // Must be called by every thread of the block (block-uniform control flow).
-__device__ __forceinline__ void q_flush(LdsQueue& q, int32_t* out, uint32_t* gcnt, int room,
+template <int CAP>
+__device__ __forceinline__ void q_flush(LdsQueueN<CAP>& q, int32_t* out, uint32_t* gcnt, int room,
                                         bool force) {
   __syncthreads();
   const uint32_t n = q.n;
   __syncthreads();
-  if (n == 0 || (!force && n + (uint32_t)room <= (uint32_t)kQCap)) return;
+  if (n == 0 || (!force && n + (uint32_t)room <= (uint32_t)CAP)) return;
   if (threadIdx.x == 0) q.base = atomicAdd(gcnt, n);
   __syncthreads();
   const uint32_t base = q.base;

@@ -583,26 +583,42 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
                                                          const int64_t* rowptr,
                                                          const uint32_t* done, int wide_deg,
                                                          int32_t* act, int32_t* actw, Ctr* ctr) {
-  __shared__ LdsQueue qn, qw;
+  // 8K-item queues (64 KB of LDS): one counter atomic per ~8 steps instead of one per step
+  // (33M vertices: 64K serialised atomics on two addresses were most of the 0.38 ms)
+  __shared__ LdsQueueN<8192> qn, qw;
   __shared__ unsigned long long scratch[kWaves];
   q_init(qn);
   q_init(qw);
   __syncthreads();
   unsigned long long eu = 0;
-  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < cnt; b += (int64_t)gridDim.x * kBlock) {
-    const int64_t j = b + threadIdx.x;
-    const int64_t i = part + j * nparts;
-    int64_t d = 0;
-    bool ok = false;
-    if (j < cnt) {
-      d = rowptr[i + 1] - rowptr[i];
-      ok = d > 0 && !is_done(done, (int32_t)i);
+  // VPT vertices per thread per step (loads first, pushes after, in ascending vertex order):
+  // the queue flushes (4 block barriers each step) are amortised over VPT*kBlock vertices
+  constexpr int VPT = 4;
+  constexpr int64_t kStep = (int64_t)VPT * kBlock;
+  for (int64_t b = (int64_t)blockIdx.x * kStep; b < cnt; b += (int64_t)gridDim.x * kStep) {
+    int64_t d[VPT];
+    uint32_t dw[VPT];
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int64_t j = b + q * kBlock + threadIdx.x;
+      const int64_t i = part + j * nparts;
+      d[q] = 0;
+      dw[q] = ~0u;
+      if (j < cnt) {
+        d[q] = rowptr[i + 1] - rowptr[i];
+        dw[q] = done[i >> 5];
+      }
     }
-    if (ok) eu += (unsigned long long)d;
-    q_push(qn, ok && d <= wide_deg, (int32_t)i);
-    q_push(qw, ok && d > wide_deg, (int32_t)i);
-    q_flush(qn, act, &ctr->act2.v, kBlock, false);
-    q_flush(qw, actw, &ctr->actw2.v, kBlock, false);
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int64_t i = part + (b + q * kBlock + threadIdx.x) * nparts;
+      const bool ok = d[q] > 0 && !((dw[q] >> (i & 31)) & 1u);
+      if (ok) eu += (unsigned long long)d[q];
+      q_push(qn, ok && d[q] <= wide_deg, (int32_t)i);
+      q_push(qw, ok && d[q] > wide_deg, (int32_t)i);
+    }
+    q_flush(qn, act, &ctr->act2.v, (int)kStep, false);
+    q_flush(qw, actw, &ctr->actw2.v, (int)kStep, false);
   }
   q_flush(qn, act, &ctr->act2.v, 0, true);
   q_flush(qw, actw, &ctr->actw2.v, 0, true);
@@ -2163,7 +2179,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
         // off only for much higher degrees, so later lists are split at a higher threshold
         const int wide0 = S.bu_levels == 0 ? opt.wide_degree : next_wide;
-        k_build_active<<<grid_for(S.cnt, kBlock), kBlock, 0, s>>>(
+        k_build_active<<<grid_for(S.cnt, 4 * kBlock), kBlock, 0, s>>>(
             S.cnt, S.part, S.nparts, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
             actw_[0].as<int32_t>(), ctr_.as<Ctr>());
         MSBFS_HIP_CHECK(hipGetLastError());

@@ -123,6 +123,8 @@ for s in "$@"; do
             step dc26 300 python bench.py --steps 3 --warmup 1 &&
             step dc30 600 python bench.py --scale 30 --groups 256 --steps 2 --warmup 1 &&
             step dcroad 600 python tools/bench_graph.py --graph grid:4896:4896:0.6 --groups 64 --steps 1 ;;
+    profhyb8) export TMPDIR=/tmp; rm -rf gpurun_out/profhyb; step profhyb8 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profhyb -o run -- python tools/hybrid_sim.py --scale 26 --ranks 8 --no-roundrobin &&
+              python tools/prof_summary.py gpurun_out/profhyb > gpurun_out/profhyb.md && rm -f gpurun_out/profhyb/run_kernel_trace.csv ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
