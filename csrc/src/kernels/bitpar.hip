@@ -1575,13 +1575,18 @@ __global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, cons
 // nw), done = every alive group present, anyvis = any bit. One thread per vertex; the bitmaps
 // are written with plain stores from wave ballots (64 vertices = 2 words), so no memset.
 // recv holds, per source part r (in order), nw words of each of r's vertices v = r + i*nparts.
+// It also builds the first phase-C level's active lists (deg > 0, not done, split at wide_deg;
+// what k_build_active would do in a second pass over the vertices). Vertices >= n_eff (no
+// edges) are skipped: no phase-C kernel reads their rows or bits.
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, int nw, int64_t n,
+__global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, int nw,
                                                          int64_t n_eff, int nparts, PartPrefix pre,
                                                          uint64_t* visA, uint64_t* visB,
                                                          const uint64_t* alive,
                                                          const uint64_t* gmask, uint32_t* done,
-                                                         uint32_t* anyvis) {
+                                                         uint32_t* anyvis, const int64_t* rowptr,
+                                                         int wide_deg, int32_t* act,
+                                                         int32_t* actw, Ctr* ctr) {
   // G lanes per vertex (the solver's row layout): every row read and write is coalesced (with one
   // thread per vertex the W-word rows were written at a W*8-byte lane stride: 6.9 ms instead of
   // ~1 ms at W = 8). A block covers TILE consecutive vertices, a multiple of 32, so it writes whole
@@ -1590,16 +1595,24 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   static_assert(TILE % 32 == 0, "whole bitmap words per block");
   __shared__ uint8_t fullf[TILE], nzf[TILE];
-  const int64_t nwords32 = (n + 31) / 32;
+  __shared__ LdsQueueN<2048> qn, qw;
+  __shared__ unsigned long long scratch[kWaves];
+  q_init(qn);
+  q_init(qw);
+  __syncthreads();
+  unsigned long long eu = 0;
+  const int64_t nwords32 = (n_eff + 31) / 32;
   const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < n; tb += (int64_t)gridDim.x * TILE) {
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < n_eff; tb += (int64_t)gridDim.x * TILE) {
     const int64_t v = tb + wv * VPW + sub;
     V<VW> x = vzero<VW>();
+    int64_t deg = 0;
     if (v < n_eff) {
       const uint64_t* src = recv + (pre.b[v % nparts] + v / nparts) * nw;
+      if (slot == 0) deg = rowptr[v + 1] - rowptr[v];
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
         const int w = slot * VW + j;
@@ -1607,7 +1620,7 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
       }
     }
     bool nz = false, full = true;
-    if (v < n) {
+    if (v < n_eff) {
       stv<VW>(visA + v * W + slot * VW, x);
       stv<VW>(visB + v * W + slot * VW, x);
 #pragma unroll
@@ -1619,10 +1632,15 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
     const bool g_nz = (__ballot(nz) >> (sub * G)) & L::GBITS;
     const bool g_full = !((__ballot(!full) >> (sub * G)) & L::GBITS);
     if (slot == 0) {
-      fullf[wv * VPW + sub] = v < n && g_full;
+      fullf[wv * VPW + sub] = v < n_eff && g_full;
       nzf[wv * VPW + sub] = g_nz;
     }
-    __syncthreads();
+    const bool actv = slot == 0 && v < n_eff && deg > 0 && !g_full;
+    if (actv) eu += (unsigned long long)deg;
+    q_push(qn, actv && deg <= wide_deg, (int32_t)v);
+    q_push(qw, actv && deg > wide_deg, (int32_t)v);
+    q_flush(qn, act, &ctr->act2.v, TILE, false);
+    q_flush(qw, actw, &ctr->actw2.v, TILE, false);
     for (int i = threadIdx.x; i < TILE / 32; i += kBlock) {
       const int64_t w32 = (tb >> 5) + i;
       if (w32 < nwords32) {
@@ -1637,6 +1655,9 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
     }
     __syncthreads();
   }
+  q_flush(qn, act, &ctr->act2.v, 0, true);
+  q_flush(qw, actw, &ctr->actw2.v, 0, true);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
 }
 
 // n_eff = 1 + the last vertex with deg > 0 (0 if none): per-thread max, wave max, one atomic
@@ -2619,7 +2640,6 @@ template <int W>
 void BitparSolver::phase_c_impl(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
                                 const uint64_t* recv, const int64_t* reduced, int64_t* F_out,
                                 RunStats* st, hipStream_t s) {
-  const int64_t n = g_.n;
   MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
   MSBFS_HIP_CHECK(hipMemsetAsync(small_.p, 0, small_.bytes, s));
   const Small sm = small();
@@ -2640,17 +2660,27 @@ void BitparSolver::phase_c_impl(int64_t K, int w_begin, int w_count, int nparts,
     PartPrefix pre{};
     for (int r = 0; r < nparts; ++r) pre.b[r + 1] = pre.b[r] + part_count(n_eff, r, nparts);
     k_hybrid_setup<W><<<grid_for(n_eff, Lay<W>::TILE, 8192), kBlock, 0, s>>>(
-        recv, w_count, n_eff, n_eff, nparts, pre, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
-        sm.alive[0], sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>());
+        recv, w_count, n_eff, nparts, pre, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
+        sm.alive[0], sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), g_.rowptr,
+        std::max(opt.wide_degree, wide_later_), act_[0].as<int32_t>(), actw_[0].as<int32_t>(),
+        ctr_.as<Ctr>());
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   Loop S;
+  {
+    // the setup built the level-3 active lists (see k_hybrid_setup)
+    const HostCtr c = read_ctr(s);
+    S.nact = c.act2;
+    S.nactw = c.actw2;
+    S.have_active = true;
+    MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
+  }
   S.cnt = n_eff;
   S.level = 2;
   S.nf = reduced[2 * K];
   S.ef = reduced[2 * K + 1];
   S.ev = reduced[2 * K + 2];
-  S.na = n;
+  S.na = S.nact + S.nactw;
   S.ea = g_.nnz;
   S.bu_levels = 1;
   S.fsrc_acc = false;
