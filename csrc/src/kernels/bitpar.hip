@@ -286,6 +286,25 @@ __global__ __launch_bounds__(kBlock) void k_zero_src_rows(const int32_t* pv, int
   }
 }
 
+// Hybrid phase A without the per-batch fill of vis_[0] (see start_batch): levels 1-2 read only
+// the rows of the sources (k_zero_src_rows), of the level-1 targets (read through the anyvis
+// guard `lzv` of the top-down kernels: a vertex no group has visited has an all-zero row, so a
+// stale row is never used), of the rank's own vertices (the level-2 pulls; zeroed in the level-2
+// read buffer here) and of level-1-visited neighbours (the pulls always filter through anyvis).
+// rows of the vertices v = part + i*nparts, i < cnt (G lanes per row, coalesced)
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_zero_part_rows(int64_t cnt, int part, int nparts,
+                                                          uint64_t* vis) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G;
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t x = t; x < cnt * G; x += stride) {
+    const int64_t v = part + (x / G) * nparts;
+    stv<VW>(vis + v * W + (x % G) * VW, vzero<VW>());
+  }
+}
+
 template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_t* pk, int64_t np,
                                                  const int64_t* rowptr, uint64_t* visA,
@@ -339,7 +358,7 @@ template <int W, bool DIFF>
 __global__ __launch_bounds__(kBlock) void k_td_expand(
     const int32_t* fl, int64_t nf, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
     const uint64_t* visCur, const uint64_t* fsrc, const uint32_t* done, uint64_t* accNext,
-    int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr) {
+    int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr, const uint32_t* lzv = nullptr) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ LdsQueue q;
@@ -367,7 +386,8 @@ __global__ __launch_bounds__(kBlock) void k_td_expand(
         } else {
           fb = ldv<VW>(fsrc + uo);
         }
-        const V<VW> r = ldv<VW>(visCur + vo);
+        // lzv: rows of never-visited vertices may be stale (lazy reset, see k_zero_part_rows)
+        const V<VW> r = (lzv && !any_visited(lzv, v)) ? vzero<VW>() : ldv<VW>(visCur + vo);
         bool any = false;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
@@ -398,7 +418,8 @@ template <int W, bool DIFF>
 __global__ __launch_bounds__(kBlock) void k_td_expand_small(
     const int32_t* fl, int64_t nf_arg, const uint32_t* nf_dev, const int64_t* rowptr,
     const int32_t* col, const uint64_t* visCur, const uint64_t* fsrc, const uint32_t* done,
-    uint64_t* accNext, int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr) {
+    uint64_t* accNext, int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr,
+    const uint32_t* lzv = nullptr) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ LdsQueue q;
@@ -434,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void k_td_expand_small(
         v = col[e];
         if (!is_done(done, v)) {
           const int64_t vo = (int64_t)v * W + slot * VW;
-          const V<VW> r = ldv<VW>(visCur + vo);
+          const V<VW> r = (lzv && !any_visited(lzv, v)) ? vzero<VW>() : ldv<VW>(visCur + vo);
           bool any = false;
 #pragma unroll
           for (int j = 0; j < VW; ++j) {
@@ -470,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
     const int32_t* touched, const int64_t* rowptr, uint64_t* visCur, uint64_t* visOld,
     uint64_t* accNext, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* fl2,
     Ctr* ctr, const int32_t* fl_old, int64_t nf_old_arg, const uint32_t* nfold_dev,
-    uint64_t* accCur_zero, uint32_t* anyvis, uint32_t* slabF) {
+    uint64_t* accCur_zero, uint32_t* anyvis, uint32_t* slabF, int lazy) {
   static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
   const int64_t nf_old = nfold_dev ? (int64_t)*nfold_dev : nf_old_arg;
   using L = Lay<W>;
@@ -506,7 +527,8 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
       v = touched[idx];
       const int64_t vo = (int64_t)v * W + slot * VW;
       const V<VW> a = ldv<VW>(accNext + vo);
-      const V<VW> r = ldv<VW>(visCur + vo);
+      // lazy: a vertex no group has visited yet may have a stale row (see k_zero_part_rows)
+      const V<VW> r = (lazy && !any_visited(anyvis, v)) ? vzero<VW>() : ldv<VW>(visCur + vo);
       V<VW> nv;
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
@@ -1738,6 +1760,7 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_NARROW_C")) narrow_c_ = atoi(x);
     if (const char* x = getenv("MSBFS_COOP")) coop_ = atoi(x);
     if (const char* x = getenv("MSBFS_GAMMA")) gamma_ = atof(x);
+    if (const char* x = getenv("MSBFS_LAZY")) lazy_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX_H")) pfx_h_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
@@ -1839,6 +1862,7 @@ class BitparSolver final : public Solver {
     std::string plan;                   // plan[level] = 'T'/'B' forces the next level
     int64_t ev_l1 = 0;                  // ev after level 1
     int64_t ef0 = 0;                    // degree sum of the sources (level-0 frontier)
+    bool lazy = false;                  // phase A: no vis_[0] fill (see k_zero_part_rows)
   };
   struct Small {
     unsigned long long* F;
@@ -1984,6 +2008,7 @@ class BitparSolver final : public Solver {
   // (ids < 458752, two blocks per CU): RMAT-26 level 2 16.8 ms vs 18.1 (1) vs 21.2 (0)
   int pfx_ = 2;
   int32_t pfx_h_ = 0;  // MSBFS_PFX_H: lower prefix bound (tuning; smaller measured slower)
+  int lazy_ = 1;        // MSBFS_LAZY=0: hybrid phase A fills vis_[0] like a normal batch
   double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
   int coop_ = -1;      // MSBFS_COOP: cross-chunk early exit on the first pull level (-1 auto)
   int narrow_c_ = 2;   // MSBFS_NARROW_C: short first narrow step (0 off, 1 always, 2 by level)
@@ -2030,7 +2055,10 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
   // Rows of vertices >= n_eff (deg 0) are never read: only sources can be there, and their rows
   // are zeroed by k_zero_src_rows. vis_[1]: see k_zero_src_rows.
   const size_t vb = (size_t)std::max<int64_t>(n_eff(), 1) * W * sizeof(uint64_t);
-  MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));
+  if (!S.lazy) MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));
+  else if (S.cnt > 0)  // hybrid phase A: only the rows levels 1-2 read (see k_zero_part_rows)
+    k_zero_part_rows<W><<<grid_for(S.cnt * Lay<W>::G, kBlock, 8192), kBlock, 0, s>>>(
+        S.cnt, S.part, S.nparts, vis_[0].as<uint64_t>());
   MSBFS_HIP_CHECK(hipMemsetAsync(done_.p, 0, done_.bytes, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(anyvis_.p, 0, anyvis_.bytes, s));
   MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
@@ -2136,6 +2164,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
     if (!bottom_up) {
       // ---- top-down
       ++epoch_;
+      const uint32_t* lzv = S.lazy ? anyvis_.as<uint32_t>() : nullptr;  // see k_zero_part_rows
       if (g_.max_degree <= kSmallDeg) {
         // low-degree graph: vertex-parallel expansion, no degree scan
         const int eg = grid_for(S.nf, L::TILE, 4096);
@@ -2144,13 +2173,13 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
               fl_[S.fc].as<int32_t>(), S.nf, nullptr, g_.rowptr, g_.col, R,
               acc_[S.ac].as<uint64_t>(),
               done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
-              touched_.as<int32_t>(), ctr_.as<Ctr>());
+              touched_.as<int32_t>(), ctr_.as<Ctr>(), lzv);
         else
           k_td_expand_small<W, true><<<eg, kBlock, 0, s>>>(
               fl_[S.fc].as<int32_t>(), S.nf, nullptr, g_.rowptr, g_.col, R, O,
               done_.as<uint32_t>(),
               acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
-              touched_.as<int32_t>(), ctr_.as<Ctr>());
+              touched_.as<int32_t>(), ctr_.as<Ctr>(), lzv);
       } else {
       frontier_degree_scan(g_.rowptr, fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(),
                            scan_tmp_.p, scan_bytes_, s);
@@ -2159,12 +2188,12 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         k_td_expand<W, false><<<eg, kBlock, 0, s>>>(
             fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R,
             acc_[S.ac].as<uint64_t>(), done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(),
-            stamp_.as<int32_t>(), epoch_, touched_.as<int32_t>(), ctr_.as<Ctr>());
+            stamp_.as<int32_t>(), epoch_, touched_.as<int32_t>(), ctr_.as<Ctr>(), lzv);
       else
         k_td_expand<W, true><<<eg, kBlock, 0, s>>>(
             fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R, O,
             done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
-            touched_.as<int32_t>(), ctr_.as<Ctr>());
+            touched_.as<int32_t>(), ctr_.as<Ctr>(), lzv);
       }
       MSBFS_HIP_CHECK(hipGetLastError());
       // touched <= min(n, frontier edges); the kernel reads the exact count from ctr
@@ -2177,7 +2206,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           touched_.as<int32_t>(), g_.rowptr, R, O, acc_[S.ac ^ 1].as<uint64_t>(), alive,
           sm.gmask, done_.as<uint32_t>(), fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
           fl_[S.fc].as<int32_t>(), S.nf, nullptr,
-          S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr, anyvis_.as<uint32_t>(), slabF(rows));
+          S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr, anyvis_.as<uint32_t>(), slabF(rows),
+          S.lazy ? 1 : 0);
       MSBFS_HIP_CHECK(hipGetLastError());
       if (fuse) {
         rows += gf;
@@ -2219,7 +2249,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
             fl_[S.fc].as<int32_t>(), S.nf, acc_[S.ac].as<uint64_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
       }
-      const bool filter = (double)S.ev < filter_frac_ * (double)g_.nnz;
+      // (lazy reset: every gathered row must be a visited one, so always filter)
+      const bool filter = S.lazy || (double)S.ev < filter_frac_ * (double)g_.nnz;
       // sparse row codes for the first bottom-up level after level 1 (see k_build_codes)
       int32_t code_from = kNoCodes;
       const uint16_t* codes = nullptr;
@@ -2238,7 +2269,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         }
       }
       // hub rows (lowest ids after degree relabelling) sized to ~hub_bytes_ are always loaded
-      const int64_t hub_ids = g_.old2new ? (int64_t)(hub_bytes_ / (8.0 * W)) : 0;
+      const int64_t hub_ids = g_.old2new && !S.lazy ? (int64_t)(hub_bytes_ / (8.0 * W)) : 0;
       const int32_t filter_from =
           filter ? (int32_t)std::min<int64_t>(hub_ids, INT32_MAX) : INT32_MAX;
       constexpr int kHubW = 14336;  // 56 KB of LDS: ids < 458752
@@ -2513,7 +2544,7 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
                                done_.as<uint32_t>(), fl_[S.fc ^ 1].as<int32_t>(), cur,
                                fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v,
                                S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr,
-                               anyvis_.as<uint32_t>(), slabF_.as<uint32_t>());
+                               anyvis_.as<uint32_t>(), slabF_.as<uint32_t>(), 0);
     if (!fuse)
       k_count_frontier<W, COUNT, false><<<grid, kBlock, 0, s>>>(
           fl_[S.fc ^ 1].as<int32_t>(), cur, g_.rowptr, acc_[S.ac ^ 1].as<uint64_t>(), nullptr,
@@ -2605,6 +2636,7 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
   S.stop_level = 2;
   S.weight_l1 = count_l1;
   S.plan = "TB";
+  S.lazy = lazy_ && fuse_count_ && opt.force_dir == 0 && dirs_.empty();
   start_batch<W, false>(0, K, qoff, qids, S, s);
   levels<W, false>(S, st, s);
   if (S.fsrc_acc && S.nf > 0) {  // stopped after a top-down level: restore the zero accumulator

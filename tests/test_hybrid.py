@@ -131,6 +131,27 @@ def test_hybrid_matches_cpu_other_graphs(msbfs_pkg, world):
 
 
 @pytest.mark.gpu
+def test_hybrid_lazy_reset_with_stale_rows(msbfs_pkg, monkeypatch):
+    """Phase A skips the visited-buffer fill (k_zero_part_rows + the top-down anyvis guard): run
+    it over buffers full of another query set's rows (a normal run, then other phases) and check
+    every result against the filled variant (MSBFS_LAZY=0) and the standard solver."""
+    m = msbfs_pkg
+    H = _H()
+    dg = m.DeviceGraph.rmat(15, 16, 11, device=0, relabel=True)
+    qa = m.QuerySet.random(dg.n, 1024, 16, seed=3)
+    qb = m.QuerySet.random(dg.n, 700, 4, seed=4)
+    with m.Solver(dg, "bitpar", max_groups=1024) as s:
+        ref_a, ref_b = s.run(qa).F, s.run(qb).F
+        for world in (8, 3, 8):
+            assert np.array_equal(H.emulate_ranks(s, qa, world), ref_a), world
+            assert np.array_equal(H.emulate_ranks(s, qb, world), ref_b), world
+        assert np.array_equal(s.run(qa).F, ref_a)
+    monkeypatch.setenv("MSBFS_LAZY", "0")
+    with m.Solver(dg, "bitpar", max_groups=1024) as s:
+        assert np.array_equal(H.emulate_ranks(s, qb, 4), ref_b)
+
+
+@pytest.mark.gpu
 def test_hybrid_runner_single_process(msbfs_pkg):
     m = msbfs_pkg
     H = _H()

@@ -125,6 +125,7 @@ for s in "$@"; do
             step dcroad 600 python tools/bench_graph.py --graph grid:4896:4896:0.6 --groups 64 --steps 1 ;;
     profhyb8) export TMPDIR=/tmp; rm -rf gpurun_out/profhyb; step profhyb8 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profhyb -o run -- python tools/hybrid_sim.py --scale 26 --ranks 8 --no-roundrobin &&
               python tools/prof_summary.py gpurun_out/profhyb > gpurun_out/profhyb.md && rm -f gpurun_out/profhyb/run_kernel_trace.csv ;;
+    lazy) for x in 1 0; do MSBFS_LAZY=$x step lazy_$x 600 python tools/hybrid_sim.py --scale 26 --ranks 4 8 --no-roundrobin || exit 1; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
