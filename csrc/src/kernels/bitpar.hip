@@ -601,23 +601,29 @@ __global__ __launch_bounds__(kBlock) void k_zero_acc(const int32_t* fl, int64_t 
 // build the bottom-up active lists (deg > 0, not done) over the vertices v = part + i*nparts,
 // i < cnt, split by degree (nparts = 1: every vertex; the hybrid mode's vertex-partitioned
 // level pulls only for its own residue class)
+template <int QCAP>
 __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, int nparts,
                                                          const int64_t* rowptr,
                                                          const uint32_t* done, int wide_deg,
                                                          int32_t* act, int32_t* actw, Ctr* ctr) {
-  // 8K-item queues (64 KB of LDS): one counter atomic per ~8 steps instead of one per step
-  // (33M vertices: 64K serialised atomics on two addresses were most of the 0.38 ms)
-  __shared__ LdsQueueN<8192> qn, qw;
+  // Each block owns QCAP consecutive list positions j and flushes its narrow queue once at the
+  // end (one counter atomic per QCAP vertices: atomics on one address serialise, and 64K of them
+  // were most of this kernel's time on 33M vertices). Blocks are dispatched in order, so the
+  // lists come out nearly ascending (hubs first in the wide list: the chunk kernel deals chunks
+  // in list order, and a grid-stride build that interleaved distant ranges cost ~1 ms of level-2
+  // tail on RMAT-26). The rare wide vertices go through a small queue flushed when needed.
+  constexpr int VPT = 4;  // vertices per thread per step (loads first, pushes after)
+  constexpr int64_t kStep = (int64_t)VPT * kBlock;
+  static_assert(QCAP % kStep == 0, "whole steps per block");
+  __shared__ LdsQueueN<QCAP> qn;
+  __shared__ LdsQueue qw;
   __shared__ unsigned long long scratch[kWaves];
   q_init(qn);
   q_init(qw);
   __syncthreads();
   unsigned long long eu = 0;
-  // VPT vertices per thread per step (loads first, pushes after, in ascending vertex order):
-  // the queue flushes (4 block barriers each step) are amortised over VPT*kBlock vertices
-  constexpr int VPT = 4;
-  constexpr int64_t kStep = (int64_t)VPT * kBlock;
-  for (int64_t b = (int64_t)blockIdx.x * kStep; b < cnt; b += (int64_t)gridDim.x * kStep) {
+  const int64_t b0 = (int64_t)blockIdx.x * QCAP, b1 = min(b0 + (int64_t)QCAP, cnt);
+  for (int64_t b = b0; b < b1; b += kStep) {
     int64_t d[VPT];
     uint32_t dw[VPT];
 #pragma unroll
@@ -626,7 +632,7 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
       const int64_t i = part + j * nparts;
       d[q] = 0;
       dw[q] = ~0u;
-      if (j < cnt) {
+      if (j < b1) {
         d[q] = rowptr[i + 1] - rowptr[i];
         dw[q] = done[i >> 5];
       }
@@ -639,7 +645,6 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
       q_push(qn, ok && d[q] <= wide_deg, (int32_t)i);
       q_push(qw, ok && d[q] > wide_deg, (int32_t)i);
     }
-    q_flush(qn, act, &ctr->act2.v, (int)kStep, false);
     q_flush(qw, actw, &ctr->actw2.v, (int)kStep, false);
   }
   q_flush(qn, act, &ctr->act2.v, 0, true);
@@ -1761,6 +1766,7 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_COOP")) coop_ = atoi(x);
     if (const char* x = getenv("MSBFS_GAMMA")) gamma_ = atof(x);
     if (const char* x = getenv("MSBFS_LAZY")) lazy_ = atoi(x);
+    if (const char* x = getenv("MSBFS_AQ")) aq_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX_H")) pfx_h_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
@@ -2008,6 +2014,7 @@ class BitparSolver final : public Solver {
   // (ids < 458752, two blocks per CU): RMAT-26 level 2 16.8 ms vs 18.1 (1) vs 21.2 (0)
   int pfx_ = 2;
   int32_t pfx_h_ = 0;  // MSBFS_PFX_H: lower prefix bound (tuning; smaller measured slower)
+  int aq_ = 4096;       // MSBFS_AQ: vertices per block of the active-list build (4096 or 1024)
   int lazy_ = 1;        // MSBFS_LAZY=0: hybrid phase A fills vis_[0] like a normal batch
   double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
   int coop_ = -1;      // MSBFS_COOP: cross-chunk early exit on the first pull level (-1 auto)
@@ -2230,7 +2237,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
         // off only for much higher degrees, so later lists are split at a higher threshold
         const int wide0 = S.bu_levels == 0 ? opt.wide_degree : next_wide;
-        k_build_active<<<grid_for(S.cnt, 4 * kBlock), kBlock, 0, s>>>(
+        auto kb = aq_ == 1024 ? k_build_active<1024> : k_build_active<4096>;
+        kb<<<grid_for(S.cnt, aq_ == 1024 ? 1024 : 4096, INT32_MAX), kBlock, 0, s>>>(
             S.cnt, S.part, S.nparts, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
             actw_[0].as<int32_t>(), ctr_.as<Ctr>());
         MSBFS_HIP_CHECK(hipGetLastError());

@@ -126,6 +126,7 @@ for s in "$@"; do
     profhyb8) export TMPDIR=/tmp; rm -rf gpurun_out/profhyb; step profhyb8 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profhyb -o run -- python tools/hybrid_sim.py --scale 26 --ranks 8 --no-roundrobin &&
               python tools/prof_summary.py gpurun_out/profhyb > gpurun_out/profhyb.md && rm -f gpurun_out/profhyb/run_kernel_trace.csv ;;
     lazy) for x in 1 0; do MSBFS_LAZY=$x step lazy_$x 600 python tools/hybrid_sim.py --scale 26 --ranks 4 8 --no-roundrobin || exit 1; done ;;
+    aq) for x in 4096 1024 4096 1024; do MSBFS_AQ=$x step aq_$x 300 python bench.py --steps 3 --warmup 1 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/aq_$x.log; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
