@@ -687,6 +687,12 @@ __global__ __launch_bounds__(kBlock) void k_build_codes(const uint64_t* R, const
   }
 }
 
+__global__ void k_mul_mask(int32_t* x, int64_t cnt, uint32_t a, uint32_t mask) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = (int32_t)(((uint32_t)x[i] * a) & mask);
+}
+
 // first id with degree < min_deg (rows relabelled by descending degree; one thread)
 __global__ void k_degree_bound(const int64_t* rowptr, int64_t n, int64_t min_deg, int32_t* out) {
   int64_t lo = 0, hi = n;
@@ -1767,6 +1773,7 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_GAMMA")) gamma_ = atof(x);
     if (const char* x = getenv("MSBFS_LAZY")) lazy_ = atoi(x);
     if (const char* x = getenv("MSBFS_AQ")) aq_ = atoi(x);
+    if (const char* x = getenv("MSBFS_SORT_ACT")) sort_act_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX_H")) pfx_h_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
@@ -2014,6 +2021,8 @@ class BitparSolver final : public Solver {
   // (ids < 458752, two blocks per CU): RMAT-26 level 2 16.8 ms vs 18.1 (1) vs 21.2 (0)
   int pfx_ = 2;
   int32_t pfx_h_ = 0;  // MSBFS_PFX_H: lower prefix bound (tuning; smaller measured slower)
+  int sort_act_ = 0;
+  DevBuf sort_tmp_;
   int aq_ = 4096;       // MSBFS_AQ: vertices per block of the active-list build (4096 or 1024)
   int lazy_ = 1;        // MSBFS_LAZY=0: hybrid phase A fills vis_[0] like a normal batch
   double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
@@ -2249,6 +2258,17 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
       }
       const bool first_bu = S.bu_levels == 0;
+      if (sort_act_ && !first_bu && S.nact > 1) {  // MSBFS_SORT_ACT (experiment): list order
+        int eb = 1;
+        while (eb < 31 && ((int64_t)1 << eb) < n) ++eb;
+        const uint32_t mask = (uint32_t)(((uint64_t)1 << eb) - 1);
+        const uint32_t a = 0x9E3779B1u, ainv = 0x0E8B2F51u;  // odd, a * ainv == 1 mod 2^32
+        if (sort_act_ == 2)
+          k_mul_mask<<<grid_for(S.nact, kBlock, 4096), kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, a, mask);
+        sort_i32_keys(act_[0].as<int32_t>(), touched_.as<int32_t>(), S.nact, eb, sort_tmp_, s);
+        if (sort_act_ == 2)
+          k_mul_mask<<<grid_for(S.nact, kBlock, 4096), kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, ainv, mask);
+      }
       ++S.bu_levels;
       if (S.fsrc_acc) {
         // bottom-up does not read frontier bits; clear the pending top-down ones so acc_[ac]
