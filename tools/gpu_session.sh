@@ -128,6 +128,8 @@ for s in "$@"; do
     lazy) for x in 1 0; do MSBFS_LAZY=$x step lazy_$x 600 python tools/hybrid_sim.py --scale 26 --ranks 4 8 --no-roundrobin || exit 1; done ;;
     aq) for x in 4096 1024 4096 1024; do MSBFS_AQ=$x step aq_$x 300 python bench.py --steps 3 --warmup 1 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/aq_$x.log; done ;;
     sortact) for x in 2 0 2 0; do MSBFS_SORT_ACT=$x step sortact_$x 300 python bench.py --steps 3 --warmup 1 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/sortact_$x.log; done ;;
+    overlap) for x in 1 0 1 0; do MSBFS_OVERLAP=$x step overlap_$x 300 python bench.py --steps 5 --warmup 2 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/overlap_$x.log; done ;;
+    overlap128) for x in 1 0; do MSBFS_OVERLAP=$x step overlap128_$x 300 python bench.py --steps 5 --warmup 2 --groups 128 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/overlap128_$x.log; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
