@@ -224,6 +224,31 @@ struct BitCounter {
       for (int d = 0; d < D; ++d) c[j][d] = 0;
     }
   }
+  // Same, into rows of STRIDE words per 64 groups. STRIDE = 65 skews the groups of different
+  // lane slots onto different LDS banks: with 64 every lane of the wave hit the bank of bit b
+  // (level-3 k_bu_narrow counted ~5e8 bank-conflict cycles; RMAT-26 levels 3 / 4 6.46 / 2.53 ->
+  // 6.22 / 2.46 ms with 65). Summing the sub-groups' counts with shuffles before one atomic per
+  // slot measured slower (a 64-step wave-uniform bit loop: 27.2 ms/step).
+  template <int STRIDE>
+  __device__ __forceinline__ void spill_strided(uint32_t* f, int slot) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      uint64_t any = 0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) any |= c[j][d];
+      const int base = (slot * VW + j) * STRIDE;
+      while (any) {
+        const int b = __ffsll((unsigned long long)any) - 1;
+        any &= any - 1;
+        uint32_t v = 0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) v |= (uint32_t)((c[j][d] >> b) & 1ull) << d;
+        atomicAdd(&f[base + b], v);
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) c[j][d] = 0;
+    }
+  }
 };
 
 // Sum the level's slab rows: block (word, row-group); lane = group bit. F += level * count
@@ -788,11 +813,13 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
   __shared__ LdsQueue qa, qf, qw;
   __shared__ unsigned long long scratch[NWV];
   __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
-  __shared__ uint32_t cnt[FUSE ? 64 * W : 1];
+  // counter rows of CR words per 64 groups, bank-skewed (see BitCounter::spill_strided)
+  constexpr int CR = 65;
+  __shared__ uint32_t cnt[FUSE ? CR * W : 1];
   if constexpr (HUBW > 0)
     for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
   if constexpr (FUSE)
-    for (int i = threadIdx.x; i < 64 * W; i += BT) cnt[i] = 0;
+    for (int i = threadIdx.x; i < CR * W; i += BT) cnt[i] = 0;
   q_init(qa);
   q_init(qf);
   q_init(qw);
@@ -955,7 +982,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     if constexpr (FUSE) {  // nw is zero for invalid lanes
       bc.add(nw);
       if (++nadd == (1 << BitCounter<VW, PFX ? 5 : 6>::D) - 1) {
-        bc.spill(cnt, slot);
+        bc.template spill_strided<CR>(cnt, slot);
         nadd = 0;
       }
     }
@@ -994,10 +1021,10 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
   if constexpr (FUSE) {
-    bc.spill(cnt, slot);
+    bc.template spill_strided<CR>(cnt, slot);
     __syncthreads();
     uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
-    for (int i = threadIdx.x; i < 64 * W; i += BT) row[i] = cnt[i];
+    for (int i = threadIdx.x; i < 64 * W; i += BT) row[i] = cnt[CR == 65 ? i + (i >> 6) : i];
   }
 }
 

@@ -130,6 +130,8 @@ for s in "$@"; do
     sortact) for x in 2 0 2 0; do MSBFS_SORT_ACT=$x step sortact_$x 300 python bench.py --steps 3 --warmup 1 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/sortact_$x.log; done ;;
     overlap) for x in 1 0 1 0; do MSBFS_OVERLAP=$x step overlap_$x 300 python bench.py --steps 5 --warmup 2 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/overlap_$x.log; done ;;
     overlap128) for x in 1 0; do MSBFS_OVERLAP=$x step overlap128_$x 300 python bench.py --steps 5 --warmup 2 --groups 128 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/overlap128_$x.log; done ;;
+    ab) for x in a b; do step ab26_$x 300 python bench.py --steps 5 --warmup 2 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/ab26_$x.log; done
+        step ab128 300 python bench.py --steps 5 --warmup 2 --groups 128 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/ab128.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
