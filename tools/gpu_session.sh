@@ -132,6 +132,11 @@ for s in "$@"; do
     overlap128) for x in 1 0; do MSBFS_OVERLAP=$x step overlap128_$x 300 python bench.py --steps 5 --warmup 2 --groups 128 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/overlap128_$x.log; done ;;
     ab) for x in a b; do step ab26_$x 300 python bench.py --steps 5 --warmup 2 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/ab26_$x.log; done
         step ab128 300 python bench.py --steps 5 --warmup 2 --groups 128 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/ab128.log ;;
+    knobs128) for kv in NONE=0 MSBFS_NARROW_C=0 MSBFS_NARROW_C=1 MSBFS_WIDE_LATER=128 MSBFS_WIDE_LATER=1024 MSBFS_FILTER_FRAC=0 MSBFS_FILTER_FRAC=2 MSBFS_COOP=1 MSBFS_GAMMA=0; do
+          n=${kv//=/_}; env "$kv" timeout -k 10 300 python bench.py --steps 5 --warmup 2 --groups 128 > gpurun_out/k128_$n.log 2>&1 || exit 1
+          echo "$kv $(grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/k128_$n.log | tr '\n' ' ')"; done ;;
+    pmclds) export TMPDIR=/tmp; rm -rf gpurun_out/pmcb3
+         step pmcb3 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SMEM --kernel-include-regex "k_bu_chunks|k_bu_narrow" --output-format csv -d gpurun_out/pmcb3 -o run -- python bench.py --steps 1 --warmup 0 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
