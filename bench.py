@@ -78,7 +78,11 @@ def main() -> int:
     qs = msbfs.QuerySet.random(g.n, args.groups, args.group_size, args.qseed)
     solver = msbfs.Solver(g, args.algo, max_groups=qs.K, alpha=args.alpha, beta=args.beta,
                           wide_degree=args.wide_degree, max_words=args.max_words)
-    hybrid_ok = ctx.world > 1 and args.algo == "bitpar" and qs.K <= solver.hybrid_max_groups()
+    # Every rank must pick the same candidates (hybrid and round-robin call different
+    # collectives), but hybrid_max_groups() depends on the free HBM each rank saw: agree on it.
+    hybrid_local = (ctx.world > 1 and args.algo == "bitpar" and ctx.world <= H.MAX_PARTS
+                    and 1 <= qs.K <= solver.hybrid_max_groups())
+    hybrid_ok = D.allreduce_max(0.0 if hybrid_local else 1.0, ctx) == 0.0
     if args.dist == "hybrid" and not hybrid_ok:
         print("bench: hybrid mode needs >1 rank, --algo bitpar and K <= one pass", file=sys.stderr)
         return 2

@@ -9,7 +9,8 @@
 //   --algo {auto,bitpar,dist,topdown,sweep,cpu}   --comm {auto,mpi,rccl,local}
 //   --gen rmat:SCALE:EF:SEED | uniform:N:M:SEED   (per-rank device generation, no broadcast)
 //   --qgen K:SIZE:SEED                            (generated query groups)
-//   --threads N (cpu algo)  --no-cache  --json  --sort-rows  --repeat R
+//   --threads N (cpu algo)  --cache (CSR sidecar, off by default like the reference's re-read;
+//   --no-cache is accepted)  --json  --sort-rows  --repeat R
 //   --dist {auto,roundrobin,hybrid}  multi-rank decomposition (auto: hybrid when > 1 rank, the
 //          bit-parallel solver and K <= one pass; see kernels/bitpar.hip "hybrid")
 #include <hip/hip_runtime.h>
@@ -38,7 +39,7 @@ struct Args {
   int numGPU = 1;
   int threads = 0;
   int repeat = 1;
-  bool cache = true, json = false, sort_rows = false;
+  bool cache = false, json = false, sort_rows = false;
 };
 
 std::vector<std::string> split(const std::string& s, char d) {
@@ -104,6 +105,7 @@ int main(int argc, char* argv[]) {
     else if (!strcmp(argv[i], "--qgen") && has) a.qgen = argv[++i];
     else if (!strcmp(argv[i], "--threads") && has) a.threads = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--repeat") && has) a.repeat = std::max(1, atoi(argv[++i]));
+    else if (!strcmp(argv[i], "--cache")) a.cache = true;
     else if (!strcmp(argv[i], "--no-cache")) a.cache = false;
     else if (!strcmp(argv[i], "--json")) a.json = true;
     else if (!strcmp(argv[i], "--sort-rows")) a.sort_rows = true;
@@ -270,10 +272,17 @@ int main(int argc, char* argv[]) {
       if (a.json) solver->opt.count_edges = true;
       MSBFS_HIP_CHECK(hipDeviceSynchronize());
     }
-    const bool hybrid = want_hybrid && K >= 1 && K <= solver->hybrid_max_groups();
+    // Every rank must take the same branch (the two modes call different collectives), but
+    // hybrid_max_groups() depends on the free HBM each rank saw when its solver was built (ranks
+    // sharing a GPU see less): agree with a MIN all-reduce of the local eligibility.
+    const bool hybrid_local = want_hybrid && K >= 1 && P <= Solver::kHybridMaxParts &&
+                              K <= solver->hybrid_max_groups();
+    const bool hybrid = comm->allreduce_min_u64(hybrid_local ? 1 : 0) == 1;
     if (a.dist == "hybrid" && !hybrid && me == 0)
-      fprintf(stderr, "msbfs: --dist hybrid needs --algo bitpar and K <= %lld; using round-robin\n",
-              (long long)(solver ? solver->hybrid_max_groups() : 0));
+      fprintf(stderr,
+              "msbfs: --dist hybrid needs --algo bitpar, <= %d ranks and K <= one pass on every "
+              "rank; using round-robin\n",
+              Solver::kHybridMaxParts);
 
     // ---- assignment: static round-robin (main.cu:304-307), or whole 64-group words (hybrid)
     std::vector<int32_t> wbeg(P + 1, 0);

@@ -137,6 +137,8 @@ class Solver {
   // words (groups) for all vertices; the remaining levels run query-partitioned. See
   // kernels/bitpar.hip "hybrid". Largest K one hybrid round supports (0: not supported).
   virtual int64_t hybrid_max_groups() const { return 0; }
+  // Largest number of ranks (vertex parts) one hybrid round supports.
+  static constexpr int kHybridMaxParts = 64;
   // Phase A. wbeg[0..nparts]: destination word split (rank j gets words [wbeg[j], wbeg[j+1]) of
   // ceil(K/64)). send_dev: cnt*wbeg[nparts] words, destination-major, cnt = own vertices.
   // out_host[2K+3]: F partial, per-group "new at level 2" flags, then frontier size / edges /

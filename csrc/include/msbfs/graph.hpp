@@ -53,9 +53,18 @@ void write_query_bin(const std::string& path, const QuerySet& q, bool force_exte
 HostCsr build_csr(const EdgeList& el, int nthreads = 0, bool stable = false);
 // Load a graph file, using/refreshing an optional binary CSR sidecar cache (<path>.csr).
 HostCsr load_graph(const std::string& path, bool use_cache, int nthreads = 0);
-void write_csr_cache(const std::string& path, const HostCsr& g, uint64_t src_size,
-                     int64_t src_mtime);
-bool read_csr_cache(const std::string& path, HostCsr& g, uint64_t src_size, int64_t src_mtime);
+// Identity of a graph file for the sidecar cache: stat fields at ns resolution + a hash of the
+// header and 64 sampled 4-KiB blocks. Plain data (no padding), compared bytewise.
+struct CsrSourceKey {
+  uint64_t size = 0, dev = 0, ino = 0;
+  int64_t mtime_ns = 0, ctime_ns = 0;
+  uint64_t sample_hash = 0;
+};
+CsrSourceKey csr_source_key(const std::string& path);
+// best-effort: returns false (and leaves no file) on any failure
+bool write_csr_cache(const std::string& path, const HostCsr& g, const CsrSourceKey& key);
+// true only for a complete cache of the same source whose payload checksum matches
+bool read_csr_cache(const std::string& path, HostCsr& g, const CsrSourceKey& key);
 
 // ---- generators (host; device twins live in kernels/gen.hip) -------------------------------
 EdgeList gen_rmat(int scale, int64_t edgefactor, uint64_t seed, double a = 0.57,

@@ -250,60 +250,166 @@ HostCsr build_csr(const EdgeList& el, int nthreads, bool stable) {
   return g;
 }
 
-static const char kCsrMagic[8] = {'M', 'S', 'B', 'F', 'S', 'C', 'R', '1'};
+// ---- CSR sidecar cache (<graph>.csr) ---------------------------------------------------------
+// Not in the reference (it re-reads the edge list every run); opt-in (`--cache`). A cache entry is
+// only used when it was built from the very same source file: the key holds the file's size,
+// device/inode, mtime and ctime with nanosecond resolution (a rewrite within the same second
+// still changes ctime_ns) and a hash of the 12-byte header plus 64 sampled 4-KiB blocks of the
+// edge list (two graphs with the same n and m differ there with overwhelming probability). The
+// payload carries its own checksum, so a truncated or corrupted cache is rejected, not used.
+static const char kCsrMagic[8] = {'M', 'S', 'B', 'F', 'S', 'C', 'R', '2'};
 
-void write_csr_cache(const std::string& path, const HostCsr& g, uint64_t src_size,
-                     int64_t src_mtime) {
-  const std::string tmp = path + ".tmp";
-  FILE* f = fopen(tmp.c_str(), "wb");
-  if (!f) return;  // cache is best-effort
-  write_all(f, kCsrMagic, 8, tmp);
-  write_all(f, &src_size, 8, tmp);
-  write_all(f, &src_mtime, 8, tmp);
-  write_all(f, &g.n, 8, tmp);
-  write_all(f, &g.m, 8, tmp);
-  write_all(f, g.rowptr.data(), 8 * g.rowptr.size(), tmp);
-  write_all(f, g.col.data(), 4 * g.col.size(), tmp);
+namespace {
+inline uint64_t mix64(uint64_t h, uint64_t x) {
+  h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+  h *= 0xFF51AFD7ED558CCDull;
+  return h ^ (h >> 33);
+}
+uint64_t hash_bytes(const uint8_t* p, size_t n, uint64_t h) {
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t x;
+    std::memcpy(&x, p + i, 8);
+    h = mix64(h, x);
+  }
+  uint64_t tail = 0;
+  if (i < n) std::memcpy(&tail, p + i, n - i);
+  return mix64(h, tail ^ ((uint64_t)n << 56));
+}
+// order-dependent hash of a large buffer, 64-MiB pieces hashed in parallel
+uint64_t hash_parallel(const void* data, size_t bytes, uint64_t seed) {
+  const size_t piece = 64ull << 20;
+  const int64_t np = (int64_t)((bytes + piece - 1) / piece);
+  std::vector<uint64_t> ph((size_t)std::max<int64_t>(np, 1), 0);
+  const uint8_t* p = (const uint8_t*)data;
+  const int T = (int)std::min<int64_t>(std::min(default_threads(), 16), np);
+  auto work = [&](int t) {
+    for (int64_t i = t; i < np; i += T) {
+      const size_t off = (size_t)i * piece;
+      ph[i] = hash_bytes(p + off, std::min(piece, bytes - off), seed + (uint64_t)i);
+    }
+  };
+  if (T <= 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+  }
+  uint64_t h = mix64(seed, bytes);
+  for (int64_t i = 0; i < np; ++i) h = mix64(h, ph[i]);
+  return h;
+}
+}  // namespace
+
+CsrSourceKey csr_source_key(const std::string& path) {
+  struct stat st;
+  if (stat(path.c_str(), &st) != 0) fail("Could not open graph file " + path);
+  CsrSourceKey k;
+  k.size = (uint64_t)st.st_size;
+  k.dev = (uint64_t)st.st_dev;
+  k.ino = (uint64_t)st.st_ino;
+  k.mtime_ns = (int64_t)st.st_mtim.tv_sec * 1000000000ll + st.st_mtim.tv_nsec;
+  k.ctime_ns = (int64_t)st.st_ctim.tv_sec * 1000000000ll + st.st_ctim.tv_nsec;
+  uint64_t h = 0x6D73626673ull;
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) fail("Could not open graph file " + path);
+  std::vector<uint8_t> buf(4096);
+  auto sample = [&](uint64_t off, size_t len) {
+    if (off >= k.size) return;
+    len = (size_t)std::min<uint64_t>(len, k.size - off);
+    if (fseeko(f, (off_t)off, SEEK_SET) != 0 || fread(buf.data(), 1, len, f) != len) {
+      fclose(f);
+      fail("read failed on " + path);
+    }
+    h = hash_bytes(buf.data(), len, mix64(h, off));
+  };
+  sample(0, 12);
+  const int kSamples = 64;
+  for (int i = 0; i < kSamples; ++i) sample(12 + (k.size > 12 ? (k.size - 12) / kSamples * i : 0), 4096);
+  if (k.size > 4096) sample(k.size - 4096, 4096);
   fclose(f);
-  rename(tmp.c_str(), path.c_str());
+  k.sample_hash = h;
+  return k;
 }
 
-bool read_csr_cache(const std::string& path, HostCsr& g, uint64_t src_size, int64_t src_mtime) {
+bool write_csr_cache(const std::string& path, const HostCsr& g, const CsrSourceKey& key) {
+  // best-effort: any failure leaves no file behind and is not an error of the load
+  static std::atomic<uint64_t> seq{0};
+  const std::string tmp = path + ".tmp." + std::to_string((long long)getpid()) + "." +
+                          std::to_string((unsigned long long)seq.fetch_add(1));
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) return false;
+  bool ok = true;
+  try {
+    const uint64_t sum = mix64(hash_parallel(g.rowptr.data(), 8 * g.rowptr.size(), 1),
+                               hash_parallel(g.col.data(), 4 * g.col.size(), 2));
+    write_all(f, kCsrMagic, 8, tmp);
+    write_all(f, &key, sizeof(key), tmp);
+    write_all(f, &g.n, 8, tmp);
+    write_all(f, &g.m, 8, tmp);
+    write_all(f, &sum, 8, tmp);
+    write_all(f, g.rowptr.data(), 8 * g.rowptr.size(), tmp);
+    write_all(f, g.col.data(), 4 * g.col.size(), tmp);
+  } catch (const Error&) {
+    ok = false;
+  }
+  if (fclose(f) != 0) ok = false;
+  if (ok && rename(tmp.c_str(), path.c_str()) != 0) ok = false;
+  if (!ok) unlink(tmp.c_str());
+  return ok;
+}
+
+bool read_csr_cache(const std::string& path, HostCsr& g, const CsrSourceKey& key) {
   FILE* f = fopen(path.c_str(), "rb");
   if (!f) return false;
   char magic[8];
-  uint64_t sz;
-  int64_t mt, n, m;
+  CsrSourceKey k;
+  int64_t n, m;
+  uint64_t sum;
   bool ok = fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kCsrMagic, 8) == 0 &&
-            fread(&sz, 8, 1, f) == 1 && fread(&mt, 8, 1, f) == 1 && fread(&n, 8, 1, f) == 1 &&
-            fread(&m, 8, 1, f) == 1 && sz == src_size && mt == src_mtime && n >= 0 && m >= 0;
+            fread(&k, sizeof(k), 1, f) == 1 && std::memcmp(&k, &key, sizeof(k)) == 0 &&
+            fread(&n, 8, 1, f) == 1 && fread(&m, 8, 1, f) == 1 && fread(&sum, 8, 1, f) == 1 &&
+            n >= 0 && m >= 0 && n < (int64_t)1 << 40 && m < (int64_t)1 << 40;
+  HostCsr c;
   if (ok) {
-    g.n = n;
-    g.m = m;
-    g.rowptr.resize(n + 1);
-    g.col.resize(2 * m);
-    ok = fread(g.rowptr.data(), 8, n + 1, f) == (size_t)(n + 1) &&
-         fread(g.col.data(), 4, 2 * m, f) == (size_t)(2 * m) && g.rowptr.back() == 2 * m;
+    c.n = n;
+    c.m = m;
+    c.rowptr.resize(n + 1);
+    c.col.resize(2 * m);
+    ok = fread(c.rowptr.data(), 8, n + 1, f) == (size_t)(n + 1) &&
+         fread(c.col.data(), 4, 2 * m, f) == (size_t)(2 * m) && fgetc(f) == EOF &&
+         c.rowptr.front() == 0 && c.rowptr.back() == 2 * m &&
+         mix64(hash_parallel(c.rowptr.data(), 8 * c.rowptr.size(), 1),
+               hash_parallel(c.col.data(), 4 * c.col.size(), 2)) == sum;
   }
   fclose(f);
+  if (ok) g = std::move(c);
   return ok;
 }
 
 HostCsr load_graph(const std::string& path, bool use_cache, int nthreads) {
-  uint64_t size = 0;
-  int64_t mtime = 0;
-  {
-    struct stat st;
-    if (stat(path.c_str(), &st) != 0) fail("Could not open graph file " + path);
-    size = (uint64_t)st.st_size;
-    mtime = (int64_t)st.st_mtime;
-  }
   HostCsr g;
   const std::string cpath = path + ".csr";
-  if (use_cache && read_csr_cache(cpath, g, size, mtime)) return g;
+  CsrSourceKey key;
+  if (use_cache) {
+    key = csr_source_key(path);
+    if (read_csr_cache(cpath, g, key)) return g;
+  }
   EdgeList el = read_edge_list_bin(path);
   g = build_csr(el, nthreads, false);
-  if (use_cache) write_csr_cache(cpath, g, size, mtime);
+  if (use_cache) {
+    el = EdgeList();
+    // the source must not have changed while it was parsed
+    CsrSourceKey after;
+    bool same = false;
+    try {
+      after = csr_source_key(path);
+      same = std::memcmp(&after, &key, sizeof(key)) == 0;
+    } catch (const Error&) {
+    }
+    if (same) write_csr_cache(cpath, g, key);
+  }
   return g;
 }
 

@@ -1603,7 +1603,7 @@ __global__ __launch_bounds__(kBlock) void k_count_frontier(const int32_t* fl, co
 // exchange (every rank sends the same number of rows); vertices >= n_eff (the deg-0 suffix of a
 // degree-relabelled graph) are not exchanged at all.
 // ---------------------------------------------------------------------------------------------
-constexpr int kMaxParts = 64;
+constexpr int kMaxParts = Solver::kHybridMaxParts;
 struct WordSplit {
   int32_t b[kMaxParts + 1];
 };

@@ -31,6 +31,9 @@ import numpy as np
 
 from . import distributed as D
 
+# Largest world size one hybrid round supports (Solver::kHybridMaxParts in csrc device.hpp).
+MAX_PARTS = 64
+
 
 def word_split(K: int, world: int) -> np.ndarray:
     """wbeg[0..world]: rank j owns 64-group words [wbeg[j], wbeg[j+1]) of ceil(K/64)."""
@@ -114,6 +117,8 @@ class HybridRunner:
         if self.K < 1 or self.K > solver.hybrid_max_groups():
             raise ValueError(f"hybrid mode handles 1..{solver.hybrid_max_groups()} groups per "
                              f"round, got {self.K}")
+        if ctx.world > MAX_PARTS:
+            raise ValueError(f"hybrid mode handles at most {MAX_PARTS} ranks, got {ctx.world}")
         self.n_eff = g.hybrid_extent()
         self.wbeg = word_split(self.K, ctx.world)
         self.idx = own_groups(self.K, self.wbeg, ctx.rank)
