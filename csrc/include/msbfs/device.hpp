@@ -177,9 +177,6 @@ std::unique_ptr<Solver> make_sweep_solver(const DeviceGraph& g);
 size_t frontier_scan_temp_bytes(int64_t max_items);
 // plain inclusive prefix sum of int64 values (hipcub); temp >= inclusive_scan_temp_bytes(cnt)
 size_t inclusive_scan_temp_bytes(int64_t max_items);
-// ascending sort of cnt non-negative ids < 2^end_bit (through tmp, result back in keys)
-void sort_i32_keys(int32_t* keys, int32_t* tmp, int64_t cnt, int end_bit, DevBuf& temp,
-                   hipStream_t s);
 void inclusive_scan_i64(const int64_t* in, int64_t* out, int64_t cnt, void* temp,
                         size_t temp_bytes, hipStream_t s);
 void frontier_degree_scan(const int64_t* rowptr, const int32_t* list, int64_t cnt, int64_t* offs,

@@ -712,12 +712,6 @@ __global__ __launch_bounds__(kBlock) void k_build_codes(const uint64_t* R, const
   }
 }
 
-__global__ void k_mul_mask(int32_t* x, int64_t cnt, uint32_t a, uint32_t mask) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt;
-       i += (int64_t)gridDim.x * blockDim.x)
-    x[i] = (int32_t)(((uint32_t)x[i] * a) & mask);
-}
-
 // first id with degree < min_deg (rows relabelled by descending degree; one thread)
 __global__ void k_degree_bound(const int64_t* rowptr, int64_t n, int64_t min_deg, int32_t* out) {
   int64_t lo = 0, hi = n;
@@ -1739,36 +1733,6 @@ __global__ void k_extent(const int64_t* rowptr, int64_t n, unsigned long long* o
 // ---------------------------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------------------------
-// Second in-order stream with fork / join events (created on first use, on the solver's
-// device): work forked onto it waits for everything queued on the main stream so far, and the
-// main stream waits for it at the join.
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t ef = nullptr, ej = nullptr;
-  SideStream() = default;
-  SideStream(const SideStream&) = delete;
-  SideStream& operator=(const SideStream&) = delete;
-  ~SideStream() {
-    if (s) (void)hipStreamDestroy(s);
-    if (ef) (void)hipEventDestroy(ef);
-    if (ej) (void)hipEventDestroy(ej);
-  }
-  hipStream_t fork(hipStream_t main) {
-    if (!s) {
-      MSBFS_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-      MSBFS_HIP_CHECK(hipEventCreateWithFlags(&ef, hipEventDisableTiming));
-      MSBFS_HIP_CHECK(hipEventCreateWithFlags(&ej, hipEventDisableTiming));
-    }
-    MSBFS_HIP_CHECK(hipEventRecord(ef, main));
-    MSBFS_HIP_CHECK(hipStreamWaitEvent(s, ef, 0));
-    return s;
-  }
-  void join(hipStream_t main) {
-    MSBFS_HIP_CHECK(hipEventRecord(ej, s));
-    MSBFS_HIP_CHECK(hipStreamWaitEvent(main, ej, 0));
-  }
-};
-
 class BitparSolver final : public Solver {
  public:
   BitparSolver(const DeviceGraph& g, int max_groups) : g_(g) {
@@ -1831,8 +1795,6 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_GAMMA")) gamma_ = atof(x);
     if (const char* x = getenv("MSBFS_LAZY")) lazy_ = atoi(x);
     if (const char* x = getenv("MSBFS_AQ")) aq_ = atoi(x);
-    if (const char* x = getenv("MSBFS_SORT_ACT")) sort_act_ = atoi(x);
-    if (const char* x = getenv("MSBFS_OVERLAP")) overlap_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX_H")) pfx_h_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
@@ -2080,12 +2042,6 @@ class BitparSolver final : public Solver {
   // (ids < 458752, two blocks per CU): RMAT-26 level 2 16.8 ms vs 18.1 (1) vs 21.2 (0)
   int pfx_ = 2;
   int32_t pfx_h_ = 0;  // MSBFS_PFX_H: lower prefix bound (tuning; smaller measured slower)
-  int sort_act_ = 0;
-  DevBuf sort_tmp_;
-  // MSBFS_OVERLAP=1: narrow and wide pulls of a level on two streams. Off: RMAT-26 level 2
-  // 15.9 ms either way, level 3 6.5 -> 7.5 ms with it (interleaved next-level lists)
-  int overlap_ = 0;
-  SideStream side_;
   int aq_ = 4096;       // MSBFS_AQ: vertices per block of the active-list build (4096 or 1024)
   int lazy_ = 1;        // MSBFS_LAZY=0: hybrid phase A fills vis_[0] like a normal batch
   double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
@@ -2321,17 +2277,6 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
       }
       const bool first_bu = S.bu_levels == 0;
-      if (sort_act_ && !first_bu && S.nact > 1) {  // MSBFS_SORT_ACT (experiment): list order
-        int eb = 1;
-        while (eb < 31 && ((int64_t)1 << eb) < n) ++eb;
-        const uint32_t mask = (uint32_t)(((uint64_t)1 << eb) - 1);
-        const uint32_t a = 0x9E3779B1u, ainv = 0x0E8B2F51u;  // odd, a * ainv == 1 mod 2^32
-        if (sort_act_ == 2)
-          k_mul_mask<<<grid_for(S.nact, kBlock, 4096), kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, a, mask);
-        sort_i32_keys(act_[0].as<int32_t>(), touched_.as<int32_t>(), S.nact, eb, sort_tmp_, s);
-        if (sort_act_ == 2)
-          k_mul_mask<<<grid_for(S.nact, kBlock, 4096), kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, ainv, mask);
-      }
       ++S.bu_levels;
       if (S.fsrc_acc) {
         // bottom-up does not read frontier bits; clear the pending top-down ones so acc_[ac]
@@ -2388,13 +2333,6 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
             stamp_.as<int32_t>(), epoch_);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
-      // MSBFS_OVERLAP: the wide half (chunk prep, chunked pulls, finalize) runs on a side
-      // stream beside the narrow pull. The vertex sets are disjoint and the shared outputs
-      // (lists, counters, done / anyvis bits) are written with atomics, so the two halves only
-      // fill each other's tails; a probe that sees another kernel's fresh anyvis bit reads a
-      // still-zero row of R (see k_bu_chunks), which keeps it exact.
-      const bool fork = overlap_ && S.nact && S.nactw;
-      hipStream_t sw = fork ? side_.fork(s) : s;
       if (S.nact) {
         if (pfx) {
           constexpr int BT = 1024;
@@ -2454,13 +2392,13 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           int64_t* cnt = scan_tmp_.as<int64_t>();
           char* t2 = (char*)scan_tmp_.p + (((size_t)S.nactw * sizeof(int64_t) + 255) & ~size_t(255));
           const size_t tb = scan_bytes_ - (size_t)(t2 - (char*)scan_tmp_.p);
-          k_prefix_chunks<<<grid_for(S.nactw, kBlock), kBlock, 0, sw>>>(
+          k_prefix_chunks<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
               actw_[0].as<int32_t>(), S.nactw, plen, cnt);
           MSBFS_HIP_CHECK(hipGetLastError());
-          inclusive_scan_i64(cnt, offs_.as<int64_t>(), S.nactw, t2, tb, sw);
+          inclusive_scan_i64(cnt, offs_.as<int64_t>(), S.nactw, t2, tb, s);
         } else {
           frontier_degree_scan(g_.rowptr, actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(),
-                               scan_tmp_.p, scan_bytes_, sw, kChunk);
+                               scan_tmp_.p, scan_bytes_, s, kChunk);
         }
         const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
         // Early exit across a vertex's chunks (coop) everywhere except on an explosive first
@@ -2473,7 +2411,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
             !pfx && first_bu && xcd_ && g_.rows_sorted && S.nactw >= 1024 && n <= INT32_MAX;
         if (!use_xcd) {
           desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
-          k_chunk_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, sw>>>(
+          k_chunk_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
               actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, plen,
               desc_.as<ChunkDesc>());
           MSBFS_HIP_CHECK(hipGetLastError());
@@ -2490,20 +2428,20 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           int64_t* seg = segb_.as<int64_t>();
           int64_t* cnt = segc_.as<int64_t>();
           int64_t* P = cnt + nf;
-          k_seg_split<<<grid_for(nf + nw, kBlock, 8192), kBlock, 0, sw>>>(
+          k_seg_split<<<grid_for(nf + nw, kBlock, 8192), kBlock, 0, s>>>(
               actw_[0].as<int32_t>(), nw, g_.rowptr, g_.col, lb, seg);
-          k_seg_counts<<<grid_for(nf, kBlock, 8192), kBlock, 0, sw>>>(seg, nw, cnt);
-          inclusive_scan_i64(cnt, P, nf, segt_.p, segt_.bytes, sw);
-          k_seg_owner<<<grid_for(nf, kBlock, 8192), kBlock, 0, sw>>>(P, nf, owner_.as<int32_t>());
-          MSBFS_HIP_CHECK(hipMemsetAsync(heads_.p, 0, heads_.bytes, sw));
+          k_seg_counts<<<grid_for(nf, kBlock, 8192), kBlock, 0, s>>>(seg, nw, cnt);
+          inclusive_scan_i64(cnt, P, nf, segt_.p, segt_.bytes, s);
+          k_seg_owner<<<grid_for(nf, kBlock, 8192), kBlock, 0, s>>>(P, nf, owner_.as<int32_t>());
+          MSBFS_HIP_CHECK(hipMemsetAsync(heads_.p, 0, heads_.bytes, s));
           MSBFS_HIP_CHECK(hipGetLastError());
           if (hub_lds && (hub_lds_ & 1))
-            k_bu_chunks_xcd<W, 256, 1024, kHubW><<<512, 1024, 0, sw>>>(
+            k_bu_chunks_xcd<W, 256, 1024, kHubW><<<512, 1024, 0, s>>>(
                 actw_[0].as<int32_t>(), nw, seg, P, owner_.as<int32_t>(), g_.col, R, alive,
                 sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, xmode_,
                 heads_.as<QHead>());
           else
-            k_bu_chunks_xcd<W, 256, 1024, 0><<<512, 1024, 0, sw>>>(
+            k_bu_chunks_xcd<W, 256, 1024, 0><<<512, 1024, 0, s>>>(
                 actw_[0].as<int32_t>(), nw, seg, P, owner_.as<int32_t>(), g_.col, R, alive,
                 sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, xmode_,
                 heads_.as<QHead>());
@@ -2512,21 +2450,21 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           // MSBFS_HUBBIG bit 1: one block per CU with a 128-KB hub bitmap (ids < 1M)
           const bool big = (hub_big_ & 2) && n > (int64_t)kHubBig * 32 * 4 && !(pfx && pfx_small);
           auto ck = big ? k_bu_chunks<W, 256, 1024, kHubBig> : k_bu_chunks<W, 256, 1024, kHubW>;
-          ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, sw>>>(
+          ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
               desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
               sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
               coop, xmode_, codes, code_from);
         } else {
           auto ck = tile_ >= 1024 ? k_bu_chunks<W, 1024, kBlock, 0>
                     : tile_ >= 512 ? k_bu_chunks<W, 512, kBlock, 0> : k_bu_chunks<W, 256, kBlock, 0>;
-          ck<<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, sw>>>(
+          ck<<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
               desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(),
               anyvis_.as<uint32_t>(), filter_from, coop, xmode_, codes, code_from);
         }
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(S.nactw, L::TILE, grid);
         auto kf = fuse ? k_bu_wide_finalize<W, COUNT, FUSE> : k_bu_wide_finalize<W, COUNT, false>;
-        kf<<<gw, kBlock, 0, sw>>>(
+        kf<<<gw, kBlock, 0, s>>>(
             actw_[0].as<int32_t>(), S.nactw, g_.rowptr, R, O, acc_[S.ac].as<uint64_t>(), alive,
             sm.gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
             ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), act_[1].as<int32_t>(), next_wide,
@@ -2534,7 +2472,6 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         MSBFS_HIP_CHECK(hipGetLastError());
         if (fuse) rows += gw;
       }
-      if (fork) side_.join(s);
       if (!fuse) {
         // new frontier bits = Wb & ~R (both still in place: the swap is below)
         const int gc = grid_for(S.nact + S.nactw, L::TILE, grid);

@@ -511,17 +511,6 @@ size_t inclusive_scan_temp_bytes(int64_t max_items) {
   return tb + 256;
 }
 
-void sort_i32_keys(int32_t* keys, int32_t* tmp, int64_t cnt, int end_bit, DevBuf& temp,
-                   hipStream_t s) {
-  if (cnt <= 1) return;
-  if (cnt > INT32_MAX) fail("sort_i32_keys: more than 2^31 items");
-  size_t tb = 0;
-  MSBFS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, keys, tmp, (int)cnt, 0, end_bit, s));
-  temp.ensure(tb);
-  MSBFS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, tb, keys, tmp, (int)cnt, 0, end_bit, s));
-  MSBFS_HIP_CHECK(hipMemcpyAsync(keys, tmp, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-}
-
 void inclusive_scan_i64(const int64_t* in, int64_t* out, int64_t cnt, void* temp,
                         size_t temp_bytes, hipStream_t s) {
   if (cnt <= 0) return;

@@ -1,0 +1,92 @@
+"""The drop-in CLI's GPU paths: device CSR upload from a graph file, every device
+algorithm, and the multi-rank decompositions (round-robin over MPI, hybrid with ranks that own
+no 64-group word) — each checked against the CPU oracle through the 7-line report and --json F.
+
+Several ranks share the box's one GPU (-gn 1), so the CLI keeps host MPI collectives (RCCL
+refuses two ranks on one device); the hybrid all-to-all then runs through alltoallv_host_u64."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MPIEXEC = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
+
+pytestmark = pytest.mark.gpu
+
+
+def _cli(m):
+    p = m.native.CLI_PATH
+    if not os.path.exists(p):
+        pytest.fail("native CLI not built (make -C csrc)")
+    return p
+
+
+def _files(tmp_path, m, K, size, seed=3):
+    g = m.Graph.rmat(12, 8, seed)
+    gp, qp = str(tmp_path / "g.bin"), str(tmp_path / "q.bin")
+    g.write(gp)
+    qs = m.QuerySet.random(g.n, K, size, seed + 4)
+    qs.write(qp)
+    return g, qs, gp, qp
+
+
+def _check(r, ref, m, ranks):
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 8, r.stdout
+    k = m.argmin_first(ref.F)
+    assert lines[2] == f"Query number (k) with minimum F value: {k + 1}"
+    assert lines[3] == f"Minimum F value: {ref.F[k]}"
+    js = json.loads(lines[7])
+    assert js["F"] == list(map(int, ref.F))
+    assert js["ranks"] == ranks
+    return js
+
+
+def _run(cmd, env=None, timeout=110):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run(cmd, capture_output=True, text=True, env=e, timeout=timeout)
+
+
+@pytest.mark.parametrize("algo", ["bitpar", "dist", "topdown", "sweep", "auto"])
+def test_cli_gpu_single_rank(tmp_path, msbfs_pkg, algo):
+    m = msbfs_pkg
+    K = 6 if algo == "sweep" else 70
+    g, qs, gp, qp = _files(tmp_path, m, K, 3)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    r = _run([_cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo", algo, "--json"],
+             {"MSBFS_NO_MPI": "1"})
+    js = _check(r, ref, m, 1)
+    assert js["traversed_edges"] == int(ref.edges.sum())
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+@pytest.mark.parametrize("ranks,K,dist", [(2, 64, "hybrid"), (3, 64, "hybrid"), (3, 130, "hybrid"),
+                                          (2, 70, "roundrobin"), (3, 64, "auto")])
+def test_cli_gpu_multi_rank(tmp_path, msbfs_pkg, ranks, K, dist):
+    """K = 64 is one word: with 2-3 ranks, ranks >= 1 own no groups in hybrid mode (phase C
+    skipped, their F slice empty) but still take part in every collective."""
+    m = msbfs_pkg
+    g, qs, gp, qp = _files(tmp_path, m, K, 4)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    r = _run([MPIEXEC, "-n", str(ranks), _cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo",
+              "bitpar", "--dist", dist, "--json"])
+    js = _check(r, ref, m, ranks)
+    assert js["comm"] == "mpi"
+    assert js["traversed_edges"] == int(ref.edges.sum())
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+def test_cli_gpu_generator_mode_multi_rank(msbfs_pkg):
+    """--gen: every rank generates the identical graph in its own HBM (no broadcast)."""
+    m = msbfs_pkg
+    r = _run([MPIEXEC, "-n", "2", _cli(m), "--gen", "rmat:11:8:5", "--qgen", "100:3:9", "-gn", "1",
+              "--json"])
+    g = m.Graph.rmat(11, 8, 5)
+    ref = m.cpu_bfs(g, m.QuerySet.random(g.n, 100, 3, 9), count_edges=True)
+    _check(r, ref, m, 2)

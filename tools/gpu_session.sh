@@ -127,9 +127,6 @@ for s in "$@"; do
               python tools/prof_summary.py gpurun_out/profhyb > gpurun_out/profhyb.md && rm -f gpurun_out/profhyb/run_kernel_trace.csv ;;
     lazy) for x in 1 0; do MSBFS_LAZY=$x step lazy_$x 600 python tools/hybrid_sim.py --scale 26 --ranks 4 8 --no-roundrobin || exit 1; done ;;
     aq) for x in 4096 1024 4096 1024; do MSBFS_AQ=$x step aq_$x 300 python bench.py --steps 3 --warmup 1 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/aq_$x.log; done ;;
-    sortact) for x in 2 0 2 0; do MSBFS_SORT_ACT=$x step sortact_$x 300 python bench.py --steps 3 --warmup 1 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/sortact_$x.log; done ;;
-    overlap) for x in 1 0 1 0; do MSBFS_OVERLAP=$x step overlap_$x 300 python bench.py --steps 5 --warmup 2 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/overlap_$x.log; done ;;
-    overlap128) for x in 1 0; do MSBFS_OVERLAP=$x step overlap128_$x 300 python bench.py --steps 5 --warmup 2 --groups 128 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/overlap128_$x.log; done ;;
     ab) for x in a b; do step ab26_$x 300 python bench.py --steps 5 --warmup 2 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/ab26_$x.log; done
         step ab128 300 python bench.py --steps 5 --warmup 2 --groups 128 || exit 1; grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/ab128.log ;;
     knobs128) for kv in NONE=0 MSBFS_NARROW_C=0 MSBFS_NARROW_C=1 MSBFS_WIDE_LATER=128 MSBFS_WIDE_LATER=1024 MSBFS_FILTER_FRAC=0 MSBFS_FILTER_FRAC=2 MSBFS_COOP=1 MSBFS_GAMMA=0; do
