@@ -80,7 +80,7 @@ def main() -> int:
                           wide_degree=args.wide_degree, max_words=args.max_words)
     # Every rank must pick the same candidates (hybrid and round-robin call different
     # collectives), but hybrid_max_groups() depends on the free HBM each rank saw: agree on it.
-    hybrid_local = (ctx.world > 1 and args.algo == "bitpar" and ctx.world <= H.MAX_PARTS
+    hybrid_local = (ctx.distributed and args.algo == "bitpar" and ctx.world <= H.MAX_PARTS
                     and 1 <= qs.K <= solver.hybrid_max_groups())
     hybrid_ok = D.allreduce_max(0.0 if hybrid_local else 1.0, ctx) == 0.0
     if args.dist == "hybrid" and not hybrid_ok:
@@ -119,7 +119,7 @@ def main() -> int:
     # otherwise decide the choice.
     cand_ms = {}
     for m in candidates:
-        for rep in range(2 if ctx.world > 1 else 1):
+        for rep in range(2 if ctx.distributed else 1):
             D.barrier(ctx)
             torch.cuda.synchronize(dev)
             t = time.perf_counter()

@@ -162,7 +162,18 @@ class RcclComm final : public Comm {
     host_->bcast_host(&id, sizeof(id), 0);
     MSBFS_HIP_CHECK(hipSetDevice(device_));
     MSBFS_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    NCCL_CHECK(ncclCommInitRank(&comm_, host_->size(), id, host_->rank()));
+    // RCCL prints a version banner on stdout at init; the report on stdout must stay the
+    // reference's 7 lines (main.cu:403-414), so the banner goes to stderr
+    fflush(stdout);
+    const int saved = dup(1);
+    if (saved >= 0) dup2(2, 1);
+    const ncclResult_t r = ncclCommInitRank(&comm_, host_->size(), id, host_->rank());
+    fflush(stdout);
+    if (saved >= 0) {
+      dup2(saved, 1);
+      close(saved);
+    }
+    NCCL_CHECK(r);
     MSBFS_HIP_CHECK(hipMalloc(&scratch_, 64));
   }
   ~RcclComm() override {
@@ -260,7 +271,10 @@ std::unique_ptr<Comm> make_world_comm(int* argc, char*** argv) {
 
 std::unique_ptr<Comm> maybe_upgrade_rccl(std::unique_ptr<Comm> host, const std::string& want,
                                          int device) {
-  if (want == "mpi" || want == "local" || host->size() == 1 || device < 0) return host;
+  // one rank: plain host comm, unless RCCL is asked for explicitly (a one-rank communicator
+  // still runs every device collective: the RCCL code paths on a one-GPU box)
+  if (want == "mpi" || want == "local" || device < 0 || (host->size() == 1 && want != "rccl"))
+    return host;
 #if defined(MSBFS_HAVE_MPI) && defined(MSBFS_HAVE_RCCL)
   // RCCL needs one rank per GPU: check (host, device) pairs are unique across the job.
   char hn[256] = {0};

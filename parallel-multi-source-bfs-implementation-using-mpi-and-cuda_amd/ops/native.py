@@ -15,7 +15,8 @@ from typing import Optional
 import numpy as np
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_DIR, "_lib", "libmsbfs.so")
+# MSBFS_LIB: load another build of the engine (A/B timing of two builds in one GPU session)
+LIB_PATH = os.environ.get("MSBFS_LIB") or os.path.join(_PKG_DIR, "_lib", "libmsbfs.so")
 CLI_PATH = os.path.join(_PKG_DIR, "_bin", "msbfs")
 
 ALGOS = {"auto": 0, "bitpar": 1, "dist": 2, "topdown": 3, "sweep": 4, "cpu": 5}

@@ -31,10 +31,13 @@ class DistContext:
     local_rank: int = 0
     device: int = -1          # GPU ordinal, -1 for CPU
     backend: str = "none"     # "nccl" (RCCL), "gloo" or "none" (single process)
+    # a one-rank process group that still goes through every collective (MSBFS_FORCE_DIST=1):
+    # exercises the RCCL code paths on a one-GPU box
+    forced: bool = False
 
     @property
     def distributed(self) -> bool:
-        return self.world > 1 and self.backend != "none"
+        return (self.world > 1 or self.forced) and self.backend != "none"
 
     def torch_device(self):
         import torch
@@ -63,7 +66,8 @@ def init_from_env(backend: Optional[str] = None, gpus_per_node: Optional[int] = 
         torch.cuda.set_device(device)
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
-    if world > 1:
+    forced = world == 1 and os.environ.get("MSBFS_FORCE_DIST") == "1"
+    if world > 1 or forced:
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29500")
@@ -71,7 +75,7 @@ def init_from_env(backend: Optional[str] = None, gpus_per_node: Optional[int] = 
             if backend == "nccl" and device >= 0:
                 kw["device_id"] = torch.device("cuda", device)
             dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
-        return DistContext(rank, world, local_rank, device, backend)
+        return DistContext(rank, world, local_rank, device, backend, forced)
     return DistContext(0, 1, 0, device, "none")
 
 

@@ -1,0 +1,38 @@
+"""bench.py's multi-GPU code paths on the one-GPU box: MSBFS_FORCE_DIST=1 makes a one-rank
+torch.distributed process group over RCCL ("nccl") that still runs every collective (barrier,
+all-reduces, the hybrid all_to_all_single), and bench.py checks each decomposition's F vector
+against the round-robin pass before timing (exit status 3 on a mismatch)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("dist", ["hybrid", "roundrobin", "auto"])
+def test_bench_forced_rccl_one_rank(dist):
+    env = dict(os.environ, MSBFS_FORCE_DIST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
+               RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--scale", "18",
+                        "--groups", "300", "--steps", "2", "--warmup", "1", "--dist", dist,
+                        "--verify", "8"],
+                       capture_output=True, text=True, env=env, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert js["n_gpus"] == 1 and js["value"] > 0
+    if dist == "hybrid":
+        assert js["config"]["parallelism"].startswith("hybrid1")
+    if dist == "auto":
+        assert set(js["config"]["candidates_ms"]) == {"roundrobin", "hybrid"}

@@ -90,3 +90,17 @@ def test_cli_gpu_generator_mode_multi_rank(msbfs_pkg):
     g = m.Graph.rmat(11, 8, 5)
     ref = m.cpu_bfs(g, m.QuerySet.random(g.n, 100, 3, 9), count_edges=True)
     _check(r, ref, m, 2)
+
+
+@pytest.mark.parametrize("dist", ["hybrid", "roundrobin"])
+def test_cli_gpu_rccl_one_rank(tmp_path, msbfs_pkg, dist):
+    """--comm rccl with one rank: the graph broadcast (ncclBroadcast), the hybrid exchange
+    (grouped ncclSend/ncclRecv) and the result reductions (ncclAllReduce) all run through a real
+    one-rank RCCL communicator — the device-collective code of the 8-GPU runs, on one GPU."""
+    m = msbfs_pkg
+    g, qs, gp, qp = _files(tmp_path, m, 200, 4)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    r = _run([MPIEXEC, "-n", "1", _cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo", "bitpar",
+              "--comm", "rccl", "--dist", dist, "--json"])
+    js = _check(r, ref, m, 1)
+    assert js["comm"] == "rccl"
