@@ -246,3 +246,30 @@ def test_bitpar_prefix_pull_tail_push(msbfs_pkg, monkeypatch):
     with m.Solver(g, "dist") as ds:
         assert np.array_equal(ds.run(sub).F, out["1"][::128])
     g.close()
+
+
+@pytest.mark.parametrize("dirs", ["", "TBBBBBBBBBBBBBBBBBBB", "TBBTBBTBBTBBTBBT", "TBTBTBTBTBTBTBTB",
+                                  "TTBBTTBBTTBB"])
+def test_bitpar_forced_direction_plans(msbfs_pkg, monkeypatch, dirs):
+    """Forced per-level direction plans (MSBFS_DIRS): push levels right after pull levels read
+    the frontier as the difference of the two visited buffers, pulls after pushes start from the
+    top-down accumulator. Runs without the edge count (the fused-count kernels) on a relabelled
+    RMAT, uniform and road-like graphs, several batches (K > 64 * W) included, and reuses the
+    solver (stale rows of the previous run must not leak)."""
+    m = msbfs_pkg
+    if dirs:
+        monkeypatch.setenv("MSBFS_DIRS", dirs)
+    dg = m.DeviceGraph.rmat(14, 16, 5, device=0)
+    hg = dg.download()  # original ids (after relabelling download() gives internal ones)
+    dg.relabel_by_degree()
+    cases = [(dg, hg, 1024), (dg, hg, 300), (dg, hg, 1500)]
+    for name, g in _graphs(m)[2:4]:
+        cases.append((g.to_device(0), g, 200))
+    for dev, host, K in cases:
+        qs = m.QuerySet.random(host.n, K, 4, seed=K)
+        ref = m.cpu_bfs(host, qs)
+        with m.Solver(dev, "bitpar", max_groups=min(K, 1024)) as s:
+            r = s.run(qs)
+            r2 = s.run(qs)
+        assert np.array_equal(r.F, ref.F), (dirs, K)
+        assert np.array_equal(r2.F, ref.F), (dirs, K)
