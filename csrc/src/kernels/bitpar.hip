@@ -682,31 +682,49 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
 // the top hubs a vertex there was reached from one or two sources, so its visited row (8*W bytes)
 // mostly holds a single set bit (RMAT-26, 1024 groups: ~1.2 bits per row below degree ~9K).
 // Gathering those rows made the level bound by Infinity-Cache traffic (rocprofv3, k_bu_chunks at
-// level 2: 44 % L2 hit rate, ~115 GB of L2 misses for 0.74e9 row gathers). code[u] (16 bit):
-// 0 = row empty, 1 + g = only group g set, kDenseCode = anything else (gathered as before). The
+// level 2: 44 % L2 hit rate, ~115 GB of L2 misses for 0.74e9 row gathers). code[u] (32 bit):
+// 0 = row empty; else bits 30-31 = number of set groups c (1-3) and bits 10*i .. 10*i+9 their
+// ids (groups < 1024); kDenseCode = anything else (gathered as before). Several slots: the
+// multi-bit rows of the mid-degree ids (RMAT-26: degree 1K-8K, 1-2 expected bits) were most of
+// the level's L2 misses (the dense rows left did not fit one XCD's 4 MB L2 next to the top hubs'
+// rows; single-slot codes 7.5 ms for the level's chunk pulls, two slots 6.9 ms). The
 // frontier's codes occupy a 64x smaller footprint than its rows, so the pulls mostly hit L2.
 // Only ids >= code_from use codes: after degree relabelling the lower ids are the hubs, whose rows
 // are dense and L2-resident. The codes live in the top-down touched buffer (unused by bottom-up
 // levels, rebuilt by every top-down level).
 // ---------------------------------------------------------------------------------------------
-constexpr uint16_t kDenseCode = 0xFFFF;
+constexpr uint32_t kDenseCode = 0xFFFFFFFFu;  // (3 slots of group 1023: never a real code)
+constexpr int kCodeSlots = 3;
+// group of slot i of a sparse code, -1 for an unused slot
+__device__ __forceinline__ int code_g(uint32_t c, int i) {
+  return i < (int)(c >> 30) ? (int)((c >> (10 * i)) & 1023u) : -1;
+}
 constexpr int32_t kNoCodes = INT32_MAX;
 
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_build_codes(const uint64_t* R, const uint32_t* anyvis,
-                                                        int64_t lo, int64_t hi, uint16_t* code) {
+                                                        int64_t lo, int64_t hi, uint32_t* code) {
   for (int64_t u = lo + (int64_t)blockIdx.x * kBlock + threadIdx.x; u < hi;
        u += (int64_t)gridDim.x * kBlock) {
-    uint16_t c = 0;
+    uint32_t c = 0;
     if (any_visited(anyvis, (int32_t)u)) {
-      int pc = 0, first = 0;
+      int pc = 0;
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        const uint64_t w = R[u * W + j];
-        if (w && pc == 0) first = j * 64 + __ffsll((unsigned long long)w) - 1;
-        pc += __popcll(w);
+        uint64_t w = R[u * W + j];
+        const int pw = __popcll(w);
+        if (pc + pw <= kCodeSlots) {  // (dense hub rows skip the bit loop)
+          while (w) {
+            const int b = __ffsll((unsigned long long)w) - 1;
+            w &= w - 1;
+            c |= (uint32_t)(j * 64 + b) << (10 * pc);
+            ++pc;
+          }
+        } else {
+          pc += pw;
+        }
       }
-      c = pc == 0 ? 0 : (pc == 1 ? (uint16_t)(1 + first) : kDenseCode);
+      c = pc == 0 ? 0u : pc <= kCodeSlots ? c | ((uint32_t)pc << 30) : kDenseCode;
     }
     code[u] = c;
   }
@@ -740,7 +758,7 @@ __global__ void k_degree_bound(const int64_t* rowptr, int64_t n, int64_t min_deg
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_push_tail(
     const int32_t* fl, int64_t nf, int32_t H, const int64_t* rowptr, const int32_t* col,
-    const uint64_t* R, const uint16_t* code, int32_t code_from, const uint32_t* done,
+    const uint64_t* R, const uint32_t* code, int32_t code_from, const uint32_t* done,
     int part, int nparts, uint64_t* acc, int32_t* stamp, int32_t epoch) {
   // 16 lanes per frontier entry, 4 entries per wave in flight (tail vertices have tens to a few
   // hundred neighbours; the lanes of an entry take consecutive row entries)
@@ -751,7 +769,7 @@ __global__ __launch_bounds__(kBlock) void k_push_tail(
   for (int64_t i = grp; i < nf; i += ngrp) {
     const int32_t u = fl[i];
     if (u < H) continue;
-    const uint32_t c = (code && u >= code_from) ? (uint32_t)code[u] : kDenseCode;
+    const uint32_t c = (code && u >= code_from) ? code[u] : kDenseCode;
     if (c == 0) continue;
     const int64_t b = rowptr[u], e = rowptr[u + 1];
     for (int64_t k = b + slot; k < e; k += PG) {
@@ -759,7 +777,10 @@ __global__ __launch_bounds__(kBlock) void k_push_tail(
       if (nparts > 1 && v % nparts != part) continue;
       if (is_done(done, v)) continue;
       if (c != kDenseCode) {
-        atomicOr((unsigned long long*)&acc[(int64_t)v * W + ((c - 1) >> 6)], 1ull << ((c - 1) & 63));
+        for (int i = 0; i < kCodeSlots; ++i) {
+          const int g = code_g(c, i);
+          if (g >= 0) atomicOr((unsigned long long*)&acc[(int64_t)v * W + (g >> 6)], 1ull << (g & 63));
+        }
       } else {
         for (int j = 0; j < W; ++j) {
           const uint64_t w = R[(int64_t)u * W + j];
@@ -1048,7 +1069,7 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
                                            const uint64_t* R, const V<Lay<W>::VW>& am,
                                            uint64_t* acc, const uint32_t* anyvis,
                                            const uint32_t* hub, int32_t filter_from, int coop,
-                                           int xmode, int32_t* lst, const uint16_t* code,
+                                           int xmode, int32_t* lst, const uint32_t* code,
                                            int32_t code_from, unsigned long long* wacc) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
@@ -1118,7 +1139,11 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
 #pragma unroll
       for (int q = 0; q < Q; ++q)
         if (cd[q] != kDenseCode) {
-          if (cd[q]) atomicOr(&wacc[(cd[q] - 1) >> 6], 1ull << ((cd[q] - 1) & 63));
+#pragma unroll
+          for (int i = 0; i < kCodeSlots; ++i) {
+            const int g = code_g(cd[q], i);
+            if (g >= 0) atomicOr(&wacc[g >> 6], 1ull << (g & 63));
+          }
           u[q] = -1;
         }
       __builtin_amdgcn_wave_barrier();
@@ -1256,7 +1281,7 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const ChunkDesc* __restrict__ desc, const int64_t* nchunks_p, const int32_t* col,
     const uint64_t* R,
     const uint64_t* alive, const uint64_t* gmask, uint64_t* acc, const uint32_t* anyvis,
-    int32_t filter_from, int coop, int xmode, const uint16_t* code, int32_t code_from) {
+    int32_t filter_from, int coop, int xmode, const uint32_t* code, int32_t code_from) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G;
   __shared__ int32_t tile[BT / 64][T];
@@ -2048,7 +2073,7 @@ class BitparSolver final : public Solver {
   int coop_ = -1;      // MSBFS_COOP: cross-chunk early exit on the first pull level (-1 auto)
   int narrow_c_ = 2;   // MSBFS_NARROW_C: short first narrow step (0 off, 1 always, 2 by level)
   int hub_big_ = 3;  // MSBFS_HUBBIG: bit 0 narrow, bit 1 chunks use a 128-KB LDS hub bitmap
-  double code_deg_ = 2.0;
+  double code_deg_ = 3.0;  // (3-slot codes: 6.58 ms level-2 chunk pulls vs 6.69 at 2.0, 6.62 at 4.0)
   std::map<int64_t, int32_t> code_bound_;
   const void* code_key_[2] = {nullptr, nullptr};
   // first id with degree < min_deg (rounded to a power of two, cached per graph); 0 when the
@@ -2289,13 +2314,13 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       const bool filter = S.lazy || (double)S.ev < filter_frac_ * (double)g_.nnz;
       // sparse row codes for the first bottom-up level after level 1 (see k_build_codes)
       int32_t code_from = kNoCodes;
-      const uint16_t* codes = nullptr;
+      const uint32_t* codes = nullptr;
       if (first_bu && S.level == 2 && codes_ && W >= 8 && S.ef0 > 0 && n <= INT32_MAX) {
         const int64_t ne = n_eff();
         code_from = (int32_t)std::min<int64_t>(
             code_bound(code_deg_ * (double)g_.nnz / (double)S.ef0), ne);
         if (code_from < ne) {
-          uint16_t* cb = touched_.as<uint16_t>() ;  // 4n bytes >= 2n
+          uint32_t* cb = touched_.as<uint32_t>();  // n entries
           k_build_codes<W><<<grid_for(ne - code_from, kBlock, 8192), kBlock, 0, s>>>(
               R, anyvis_.as<uint32_t>(), code_from, ne, cb);
           MSBFS_HIP_CHECK(hipGetLastError());
