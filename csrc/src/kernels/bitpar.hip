@@ -702,10 +702,14 @@ __device__ __forceinline__ int code_g(uint32_t c, int i) {
 constexpr int32_t kNoCodes = INT32_MAX;
 
 template <int W>
+// ids [lo, hi), then the list entries fl[0..nl) >= hi
 __global__ __launch_bounds__(kBlock) void k_build_codes(const uint64_t* R, const uint32_t* anyvis,
-                                                        int64_t lo, int64_t hi, uint32_t* code) {
-  for (int64_t u = lo + (int64_t)blockIdx.x * kBlock + threadIdx.x; u < hi;
-       u += (int64_t)gridDim.x * kBlock) {
+                                                        int64_t lo, int64_t hi, const int32_t* fl,
+                                                        int64_t nl, uint32_t* code) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < hi - lo + nl;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t u = i < hi - lo ? lo + i : (int64_t)fl[i - (hi - lo)];
+    if (i >= hi - lo && u < hi) continue;
     uint32_t c = 0;
     if (any_visited(anyvis, (int32_t)u)) {
       int pc = 0;
@@ -2312,23 +2316,6 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       }
       // (lazy reset: every gathered row must be a visited one, so always filter)
       const bool filter = S.lazy || (double)S.ev < filter_frac_ * (double)g_.nnz;
-      // sparse row codes for the first bottom-up level after level 1 (see k_build_codes)
-      int32_t code_from = kNoCodes;
-      const uint32_t* codes = nullptr;
-      if (first_bu && S.level == 2 && codes_ && W >= 8 && S.ef0 > 0 && n <= INT32_MAX) {
-        const int64_t ne = n_eff();
-        code_from = (int32_t)std::min<int64_t>(
-            code_bound(code_deg_ * (double)g_.nnz / (double)S.ef0), ne);
-        if (code_from < ne) {
-          uint32_t* cb = touched_.as<uint32_t>();  // n entries
-          k_build_codes<W><<<grid_for(ne - code_from, kBlock, 8192), kBlock, 0, s>>>(
-              R, anyvis_.as<uint32_t>(), code_from, ne, cb);
-          MSBFS_HIP_CHECK(hipGetLastError());
-          codes = cb;
-        } else {
-          code_from = kNoCodes;
-        }
-      }
       // hub rows (lowest ids after degree relabelling) sized to ~hub_bytes_ are always loaded
       const int64_t hub_ids = g_.old2new && !S.lazy ? (int64_t)(hub_bytes_ / (8.0 * W)) : 0;
       const int32_t filter_from =
@@ -2349,6 +2336,27 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       const bool pfx = pfx_ && first_bu && S.level == 2 && hub_lds && (hub_lds_ & 3) == 3 &&
                        (pfx_small || (hub_big_ & 3) == 3) && n > (int64_t)kHubBig * 32 * 4 &&
                        g_.rows_sorted && n <= INT32_MAX;
+      // sparse row codes for the first bottom-up level after level 1 (see k_build_codes). With
+      // the prefix pull only ids < H and the tail pushers' own codes are ever read: the codes of
+      // [code_from, H) plus those of the frontier vertices >= H (not 4 bytes for every id).
+      int32_t code_from = kNoCodes;
+      const uint32_t* codes = nullptr;
+      if (first_bu && S.level == 2 && codes_ && W >= 8 && S.ef0 > 0 && n <= INT32_MAX) {
+        const int64_t ne = n_eff();
+        code_from = (int32_t)std::min<int64_t>(
+            code_bound(code_deg_ * (double)g_.nnz / (double)S.ef0), ne);
+        if (code_from < ne) {
+          uint32_t* cb = touched_.as<uint32_t>();  // n entries
+          const int64_t hi = pfx ? std::min<int64_t>(std::max<int64_t>(kPfxH, code_from), ne) : ne;
+          const int64_t nl = pfx ? S.nf : 0;
+          k_build_codes<W><<<grid_for(hi - code_from + nl, kBlock, 8192), kBlock, 0, s>>>(
+              R, anyvis_.as<uint32_t>(), code_from, hi, fl_[S.fc].as<int32_t>(), nl, cb);
+          MSBFS_HIP_CHECK(hipGetLastError());
+          codes = cb;
+        } else {
+          code_from = kNoCodes;
+        }
+      }
       const int32_t* plen = pfx ? prefix_lens(kPfxH, s) : nullptr;
       if (pfx) {
         ++epoch_;
