@@ -820,8 +820,9 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
     int next_wide, uint32_t* slabF, uint64_t* pacc, const int32_t* stamp, int32_t epoch,
-    const int32_t* plen) {
+    const int32_t* plen, const uint32_t* nact_dev) {
   static_assert(!PFX || HUBW > 0, "the prefix pull relies on the LDS hub bitmap");
+  if (nact_dev) nact = (int64_t)*nact_dev;  // (list length known only on the device)
   static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
@@ -1046,6 +1047,103 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
     for (int i = threadIdx.x; i < 64 * W; i += BT) row[i] = cnt[CR == 65 ? i + (i >> 6) : i];
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Late pull levels, first pass: from the third bottom-up level on almost every
+// active vertex is covered by its first neighbour (rows sorted: the biggest hub first), and the
+// level is bound by the latency of its dependent loads (list entry -> row offsets -> first column
+// id -> neighbour row). This lean kernel (no multi-step loop, no software pipeline) keeps few
+// registers, so twice as many waves hide that latency. A vertex the first row covers is
+// finished here exactly as k_bu_narrow would (row, counts, done bit, frontier, anyvis); the others
+// go to an overflow list (ctr->touched, unused by pull levels) that k_bu_narrow then processes
+// from scratch.
+// ---------------------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(kBlock, 8) void k_bu_first(
+    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
+    int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  constexpr int CR = 65;  // bank-skewed counter rows (see BitCounter::spill_strided)
+  __shared__ LdsQueue qo, qf;
+  __shared__ unsigned long long scratch[kWaves];
+  __shared__ uint32_t cnt[CR * W];
+  for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
+  q_init(qo);
+  q_init(qf);
+  __syncthreads();
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  unsigned long long ef = 0, ev = 0;
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nact; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t idx = tb + wv * VPW + sub;
+    const bool valid = idx < nact;
+    int32_t v = 0;
+    V<VW> r = vzero<VW>(), nw = vzero<VW>();
+    uint32_t deg = 0;
+    bool open = false, rnz = false;
+    if (valid) {
+      v = act[idx];
+      const int64_t b = rowptr[v];
+      deg = (uint32_t)(rowptr[v + 1] - b);
+      r = ldv<VW>(R + (int64_t)v * W + slot * VW);
+      const int32_t u = col[b];  // active vertices have deg > 0
+      const V<VW> x = ldv<VW>(R + (int64_t)u * W + slot * VW);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        const uint64_t unv = ~r.w[j] & am.w[j];
+        nw.w[j] = x.w[j] & unv;
+        open |= (unv & ~nw.w[j]) != 0;
+        rnz |= r.w[j] != 0;
+      }
+    }
+    const bool g_open = (__ballot(open) >> (sub * G)) & L::GBITS;
+    const bool fin = valid && !g_open;  // covered by the first row: finished at this level
+    if (!fin) nw = vzero<VW>();
+    if (fin) {
+      V<VW> nv;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
+      stv<VW>(Wb + (int64_t)v * W + slot * VW, nv);
+    }
+    bc.add(nw);
+    if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+      bc.template spill_strided<CR>(cnt, slot);
+      nadd = 0;
+    }
+    bool anynew = false;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) anynew |= nw.w[j] != 0;
+    const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
+    const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
+    const bool leader = valid && slot == 0;
+    if (leader && fin) set_done(done, v);
+    if (leader && g_new) ef += deg;
+    if (leader && g_first) {
+      atomicOr(&anyvis[v >> 5], 1u << (v & 31));
+      ev += deg;
+    }
+    q_push(qo, leader && !fin, v);
+    q_push(qf, leader && g_new, v);
+    q_flush(qo, ovf, &ctr->touched.v, TILE, false);
+    q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
+  }
+  q_flush(qo, ovf, &ctr->touched.v, 0, true);
+  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
+  bc.template spill_strided<CR>(cnt, slot);
+  __syncthreads();
+  uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+  for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
 }
 
 // bottom-up, wide vertices, phase 1: one wave per edge chunk (<= kChunk edges), processed in
@@ -1817,6 +1915,7 @@ class BitparSolver final : public Solver {
     if (const char* f = getenv("MSBFS_FUSE_COUNT")) fuse_count_ = atoi(f);
     if (const char* x = getenv("MSBFS_XCD")) xcd_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
+    if (const char* x = getenv("MSBFS_LEAN")) lean_ = atoi(x);
     if (const char* x = getenv("MSBFS_HUBBIG")) hub_big_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX")) pfx_ = atoi(x);
     if (const char* x = getenv("MSBFS_NARROW_C")) narrow_c_ = atoi(x);
@@ -2063,6 +2162,10 @@ class BitparSolver final : public Solver {
   // sparse row codes on the first bottom-up level (MSBFS_CODES=0: off); ids with degree >=
   // code_deg_ * nnz / (source degree sum), i.e. expected >= code_deg_ set bits, keep row gathers
   int codes_ = 1;
+  // lean first pass on the third and later pull levels (see k_bu_first; MSBFS_LEAN=0: off).
+  // RMAT-26, 1024 groups: level 4 2.48 -> 2.07 ms (98 % of its vertices finish on the first
+  // row); on the second pull level most vertices overflow (128 groups: level 3 3.5 -> 4.1 ms)
+  int lean_ = 1;
   DevBuf plen_;
   const void* plen_key_[2] = {nullptr, nullptr};
   int32_t plen_h_ = 0;
@@ -2379,7 +2482,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
                                next_wide, slabF(rows), acc_[S.ac].as<uint64_t>(),
-                               stamp_.as<int32_t>(), epoch_, plen);
+                               stamp_.as<int32_t>(), epoch_, plen, nullptr);
           if (fuse) rows += gn;
         } else if (hub_lds && (hub_lds_ & 2)) {
           constexpr int BT = 1024;
@@ -2395,7 +2498,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                               next_wide, slabF(rows), nullptr, nullptr, 0, nullptr);
+                               next_wide, slabF(rows), nullptr, nullptr, 0, nullptr, nullptr);
           if (fuse) rows += gn;
         } else {
           const int gn = grid_for(S.nact, L::TILE, grid);
@@ -2406,6 +2509,23 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           // 4 3.1 -> 2.5 ms; level 3 prefers full steps: 6.5 vs 6.7 ms). MSBFS_NARROW_C: 0 off,
           // 1 always, 2 (default) this rule
           const bool short1 = narrow_c_ == 1 || (narrow_c_ == 2 && (S.bu_levels >= 3 || W <= 4));
+          if (lean_ && fuse && !filt && S.bu_levels >= 3 && S.nact >= (1 << 20)) {
+            // lean first pass, then the regular pull over the vertices it could not finish
+            const int gl = grid_for(S.nact, L::TILE, grid);
+            k_bu_first<W><<<gl, kBlock, 0, s>>>(
+                act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+                done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+                ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF(rows));
+            MSBFS_HIP_CHECK(hipGetLastError());
+            rows += gl;
+            k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
+                touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+                done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+                ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+                next_wide, slabF(rows), nullptr, nullptr, 0, nullptr, &ctr_.as<Ctr>()->touched.v);
+            MSBFS_HIP_CHECK(hipGetLastError());
+            rows += gn;
+          } else {
           auto kn = fuse ? (filt ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, true>
                                  : short1 ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1>
                                           : k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false>)
@@ -2415,8 +2535,9 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                    sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                    fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                    anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                                   next_wide, slabF(rows), nullptr, nullptr, 0, nullptr);
+                                   next_wide, slabF(rows), nullptr, nullptr, 0, nullptr, nullptr);
           if (fuse) rows += gn;
+          }
         }
         MSBFS_HIP_CHECK(hipGetLastError());
       }
