@@ -311,11 +311,17 @@ __global__ __launch_bounds__(kBlock) void k_zero_src_rows(const int32_t* pv, int
   }
 }
 
-// Hybrid phase A without the per-batch fill of vis_[0] (see start_batch): levels 1-2 read only
-// the rows of the sources (k_zero_src_rows), of the level-1 targets (read through the anyvis
-// guard `lzv` of the top-down kernels: a vertex no group has visited has an all-zero row, so a
-// stale row is never used), of the rank's own vertices (the level-2 pulls; zeroed in the level-2
-// read buffer here) and of level-1-visited neighbours (the pulls always filter through anyvis).
+// Lazy batches (every batch of the fused-count path and the hybrid phase A): no per-batch fill of
+// vis_[0]. Until the first pull level a row is read only if its vertex is visited: the sources'
+// rows (k_zero_src_rows), top-down targets and touched vertices through the anyvis guard (`lzv`,
+// k_td_finalize's `lazy`: a vertex no group has visited has an all-zero row, so a stale row is
+// never used). The first pull level filters every probe and reads its own rows through a
+// snapshot of anyvis taken at the level start (k_bu_narrow `snap`), and writes the rows of all its
+// active vertices; a top-down level right after it reads the old rows through the same snapshot
+// (k_td_expand `osnap`). From then on both buffers hold valid rows for every vertex a kernel
+// reads (a vertex finished at the first pull level and first visited there keeps a stale row in
+// the other buffer, but no active vertex two levels later is its neighbour). Phase A with
+// several parts instead zeroes its own rows here (its pulls cover only them).
 // rows of the vertices v = part + i*nparts, i < cnt (G lanes per row, coalesced)
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_zero_part_rows(int64_t cnt, int part, int nparts,
@@ -383,7 +389,8 @@ template <int W, bool DIFF>
 __global__ __launch_bounds__(kBlock) void k_td_expand(
     const int32_t* fl, int64_t nf, const int64_t* offs, const int64_t* rowptr, const int32_t* col,
     const uint64_t* visCur, const uint64_t* fsrc, const uint32_t* done, uint64_t* accNext,
-    int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr, const uint32_t* lzv = nullptr) {
+    int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr, const uint32_t* lzv = nullptr,
+    const uint32_t* osnap = nullptr) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ LdsQueue q;
@@ -405,7 +412,10 @@ __global__ __launch_bounds__(kBlock) void k_td_expand(
         const int64_t uo = (int64_t)u * W + slot * VW, vo = (int64_t)v * W + slot * VW;
         V<VW> fb = ldv<VW>(visCur + uo);
         if constexpr (DIFF) {
-          const V<VW> old = ldv<VW>(fsrc + uo);
+          // osnap: the old row of a vertex first visited at the previous (first, unfilled) pull
+          // level was never written: it is all zero (see start_batch)
+          const V<VW> old =
+              (osnap && !any_visited(osnap, u)) ? vzero<VW>() : ldv<VW>(fsrc + uo);
 #pragma unroll
           for (int j = 0; j < VW; ++j) fb.w[j] &= ~old.w[j];
         } else {
@@ -444,7 +454,7 @@ __global__ __launch_bounds__(kBlock) void k_td_expand_small(
     const int32_t* fl, int64_t nf_arg, const uint32_t* nf_dev, const int64_t* rowptr,
     const int32_t* col, const uint64_t* visCur, const uint64_t* fsrc, const uint32_t* done,
     uint64_t* accNext, int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr,
-    const uint32_t* lzv = nullptr) {
+    const uint32_t* lzv = nullptr, const uint32_t* osnap = nullptr) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ LdsQueue q;
@@ -464,7 +474,8 @@ __global__ __launch_bounds__(kBlock) void k_td_expand_small(
       const int64_t uo = (int64_t)u * W + slot * VW;
       if constexpr (DIFF) {
         fb = ldv<VW>(visCur + uo);
-        const V<VW> old = ldv<VW>(fsrc + uo);
+        const V<VW> old =
+            (osnap && !any_visited(osnap, u)) ? vzero<VW>() : ldv<VW>(fsrc + uo);  // see k_td_expand
 #pragma unroll
         for (int j = 0; j < VW; ++j) fb.w[j] &= ~old.w[j];
       } else {
@@ -820,8 +831,12 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
     int next_wide, uint32_t* slabF, uint64_t* pacc, const int32_t* stamp, int32_t epoch,
-    const int32_t* plen, const uint32_t* nact_dev) {
+    const int32_t* plen, const uint32_t* nact_dev, const uint32_t* snap) {
   static_assert(!PFX || HUBW > 0, "the prefix pull relies on the LDS hub bitmap");
+  // snap (first pull level of a batch that did not clear its visited buffer, see start_batch):
+  // the any-visited bitmap as of the level start. Probes read it (a vertex first visited during
+  // this level may still have a stale row) and an own row it does not mark is all zero.
+  const uint32_t* pvis = snap ? snap : anyvis;
   if (nact_dev) nact = (int64_t)*nact_dev;  // (list length known only on the device)
   static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
   using L = Lay<W>;
@@ -838,7 +853,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
   constexpr int CR = PFX ? 64 : 65;
   __shared__ uint32_t cnt[FUSE ? CR * W : 1];
   if constexpr (HUBW > 0)
-    for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
+    for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = pvis[i];
   if constexpr (FUSE)
     for (int i = threadIdx.x; i < CR * W; i += BT) cnt[i] = 0;
   q_init(qa);
@@ -867,7 +882,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
   if (tb + stride + lofs < nact) v2 = act[tb + stride + lofs];
   uint32_t p1 = 0;  // PFX: prefix length of v1's row (ids < H)
   if (tb + lofs < nact) {
-    r1 = ldv<VW>(R + (int64_t)v1 * W + slot * VW);
+    r1 = (snap && !any_visited(snap, v1)) ? vzero<VW>() : ldv<VW>(R + (int64_t)v1 * W + slot * VW);
     b1 = rowptr[v1];
     d1 = (uint32_t)(rowptr[v1 + 1] - b1);
     if constexpr (PFX) p1 = (uint32_t)plen[v1];
@@ -890,7 +905,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
     // prefetch: row / offsets of the next tile, list entry of the one after
     v1 = v2;
     if (idx + stride < nact) {
-      r1 = ldv<VW>(R + (int64_t)v1 * W + slot * VW);
+      r1 = (snap && !any_visited(snap, v1)) ? vzero<VW>() : ldv<VW>(R + (int64_t)v1 * W + slot * VW);
       b1 = rowptr[v1];
       d1 = (uint32_t)(rowptr[v1 + 1] - b1);
       if constexpr (PFX) p1 = (uint32_t)plen[v1];
@@ -956,7 +971,7 @@ __global__ __launch_bounds__(BT, 4) void k_bu_narrow(
 #pragma unroll
           for (int q = 0; q < Q; ++q) {
             pg[q] = ~0u;
-            if (u[q] >= filter_from && !(HUBW > 0 && u[q] < HUBW * 32)) pg[q] = anyvis[u[q] >> 5];
+            if (u[q] >= filter_from && !(HUBW > 0 && u[q] < HUBW * 32)) pg[q] = pvis[u[q] >> 5];
           }
 #pragma unroll
           for (int q = 0; q < Q; ++q) {
@@ -1172,13 +1187,14 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
                                            uint64_t* acc, const uint32_t* anyvis,
                                            const uint32_t* hub, int32_t filter_from, int coop,
                                            int xmode, int32_t* lst, const uint32_t* code,
-                                           int32_t code_from, unsigned long long* wacc) {
+                                           int32_t code_from, unsigned long long* wacc,
+                                           const uint32_t* snap) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
   constexpr int PB = VW == 2 ? 4 : 8;  // rows in flight per lane group in phase B
   const int lane = lane_id(), slot = lane % G, sub = lane / G;
   const int64_t vo = (int64_t)v * W + slot * VW;
-  const V<VW> r = ldv<VW>(R + vo);
+  const V<VW> r = (snap && !any_visited(snap, v)) ? vzero<VW>() : ldv<VW>(R + vo);  // see k_bu_narrow
   // g = bits the vertex's other chunks have published so far. Chunks of one hub run
   // concurrently, so each tile publishes its partial OR with a RETURNING atomicOr that also
   // hands back the current union from the memory side (atomics bypass the non-coherent per-XCD
@@ -1383,12 +1399,14 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const ChunkDesc* __restrict__ desc, const int64_t* nchunks_p, const int32_t* col,
     const uint64_t* R,
     const uint64_t* alive, const uint64_t* gmask, uint64_t* acc, const uint32_t* anyvis,
-    int32_t filter_from, int coop, int xmode, const uint32_t* code, int32_t code_from) {
+    int32_t filter_from, int coop, int xmode, const uint32_t* code, int32_t code_from,
+    const uint32_t* snap) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G;
   __shared__ int32_t tile[BT / 64][T];
   __shared__ unsigned long long wacc[BT / 64][W];
   __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
+  if (snap) anyvis = snap;  // probes read the level-start bitmap (see k_bu_narrow)
   if constexpr (HUBW > 0) {
     for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
     __syncthreads();
@@ -1416,7 +1434,7 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const int64_t lim = beg + uni32(d.len);
     if (c + cstep < cend) d = desc[c + cstep];  // next descriptor, in flight during the pull
     chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop, xmode,
-                           lst, code, code_from, wacc[threadIdx.x >> 6]);
+                           lst, code, code_from, wacc[threadIdx.x >> 6], snap);
   }
 }
 
@@ -1546,7 +1564,7 @@ __global__ __launch_bounds__(BT) void k_bu_chunks_xcd(
         const int64_t beg = uni64(seg[f]) + j0 * kChunk;
         const int64_t lim = min(uni64(seg[f + nw]), beg + (int64_t)kChunk);
         chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, 0, xmode,
-                               lst, nullptr, kNoCodes, wacc[threadIdx.x >> 6]);
+                               lst, nullptr, kNoCodes, wacc[threadIdx.x >> 6], nullptr);
       }
     }
   }
@@ -1567,7 +1585,8 @@ template <int W, bool COUNT, bool FUSE>
 __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, uint64_t* Wb,
     uint64_t* acc, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* actw2,
-    int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* act2n, int next_wide, uint32_t* slabF) {
+    int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* act2n, int next_wide, uint32_t* slabF,
+    const uint32_t* snap) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ LdsQueue qa, qf, qn;
@@ -1598,7 +1617,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     if (valid) {
       v = wl[idx];
       const int64_t vo = (int64_t)v * W + slot * VW;
-      const V<VW> r = ldv<VW>(R + vo);
+      const V<VW> r = (snap && !any_visited(snap, v)) ? vzero<VW>() : ldv<VW>(R + vo);
       const V<VW> a = ldv<VW>(acc + vo);
       V<VW> nv;
 #pragma unroll
@@ -1888,6 +1907,7 @@ class BitparSolver final : public Solver {
     MSBFS_HIP_CHECK(hipMemset(stamp_.p, 0xFF, stamp_.bytes));
     done_.alloc((size_t)((n + 31) / 32) * sizeof(uint32_t));
     anyvis_.alloc((size_t)((n + 31) / 32) * sizeof(uint32_t));
+    asnap_.alloc((size_t)((n + 31) / 32) * sizeof(uint32_t));
     if (const char* f = getenv("MSBFS_FILTER_FRAC")) filter_frac_ = atof(f);
     if (const char* h = getenv("MSBFS_HUB_MB")) hub_bytes_ = atof(h) * (1 << 20);
     for (int i = 0; i < 2; ++i) {
@@ -2024,7 +2044,8 @@ class BitparSolver final : public Solver {
     std::string plan;                   // plan[level] = 'T'/'B' forces the next level
     int64_t ev_l1 = 0;                  // ev after level 1
     int64_t ef0 = 0;                    // degree sum of the sources (level-0 frontier)
-    bool lazy = false;                  // phase A: no vis_[0] fill (see k_zero_part_rows)
+    bool lazy = false;                  // no vis_[0] fill (see start_batch)
+    bool osnap_next = false;            // the previous level was the first pull of a lazy batch
   };
   struct Small {
     unsigned long long* F;
@@ -2175,7 +2196,8 @@ class BitparSolver final : public Solver {
   int pfx_ = 2;
   int32_t pfx_h_ = 0;  // MSBFS_PFX_H: lower prefix bound (tuning; smaller measured slower)
   int aq_ = 4096;       // MSBFS_AQ: vertices per block of the active-list build (4096 or 1024)
-  int lazy_ = 1;        // MSBFS_LAZY=0: hybrid phase A fills vis_[0] like a normal batch
+  int lazy_ = 1;        // MSBFS_LAZY=0: every batch fills vis_[0] (see start_batch)
+  DevBuf asnap_;        // any-visited bitmap at the start of a lazy batch's first pull level
   double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
   int coop_ = -1;      // MSBFS_COOP: cross-chunk early exit on the first pull level (-1 auto)
   int narrow_c_ = 2;   // MSBFS_NARROW_C: short first narrow step (0 off, 1 always, 2 by level)
@@ -2223,7 +2245,7 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
   // are zeroed by k_zero_src_rows. vis_[1]: see k_zero_src_rows.
   const size_t vb = (size_t)std::max<int64_t>(n_eff(), 1) * W * sizeof(uint64_t);
   if (!S.lazy) MSBFS_HIP_CHECK(hipMemsetAsync(vis_[0].p, 0, vb, s));
-  else if (S.cnt > 0)  // hybrid phase A: only the rows levels 1-2 read (see k_zero_part_rows)
+  else if (S.cnt > 0 && S.nparts > 1)  // hybrid phase A: only the rows levels 1-2 read (see k_zero_part_rows)
     k_zero_part_rows<W><<<grid_for(S.cnt * Lay<W>::G, kBlock, 8192), kBlock, 0, s>>>(
         S.cnt, S.part, S.nparts, vis_[0].as<uint64_t>());
   MSBFS_HIP_CHECK(hipMemsetAsync(done_.p, 0, done_.bytes, s));
@@ -2346,7 +2368,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
               fl_[S.fc].as<int32_t>(), S.nf, nullptr, g_.rowptr, g_.col, R, O,
               done_.as<uint32_t>(),
               acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
-              touched_.as<int32_t>(), ctr_.as<Ctr>(), lzv);
+              touched_.as<int32_t>(), ctr_.as<Ctr>(), lzv,
+              S.osnap_next ? asnap_.as<uint32_t>() : nullptr);
       } else {
       frontier_degree_scan(g_.rowptr, fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(),
                            scan_tmp_.p, scan_bytes_, s);
@@ -2360,7 +2383,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         k_td_expand<W, true><<<eg, kBlock, 0, s>>>(
             fl_[S.fc].as<int32_t>(), S.nf, offs_.as<int64_t>(), g_.rowptr, g_.col, R, O,
             done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
-            touched_.as<int32_t>(), ctr_.as<Ctr>(), lzv);
+            touched_.as<int32_t>(), ctr_.as<Ctr>(), lzv,
+            S.osnap_next ? asnap_.as<uint32_t>() : nullptr);
       }
       MSBFS_HIP_CHECK(hipGetLastError());
       // touched <= min(n, frontier edges); the kernel reads the exact count from ctr
@@ -2389,6 +2413,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       }
       S.ac ^= 1;
       S.fsrc_acc = true;
+      S.osnap_next = false;
       if (st) st->td_levels++;
     } else {
       // ---- bottom-up
@@ -2417,8 +2442,18 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
             fl_[S.fc].as<int32_t>(), S.nf, acc_[S.ac].as<uint64_t>());
         MSBFS_HIP_CHECK(hipGetLastError());
       }
-      // (lazy reset: every gathered row must be a visited one, so always filter)
-      const bool filter = S.lazy || (double)S.ev < filter_frac_ * (double)g_.nnz;
+      // lazy batch, first pull level: rows of vertices nobody visited yet may be stale, so every
+      // gathered row must be one of a visited vertex (always filter), and probes / own rows use a
+      // snapshot of the any-visited bitmap (a vertex first visited during the level may be
+      // probed before its row is written). From the next pull level on the read buffer holds
+      // this level's rows, valid for every vertex a pull can reach (see start_batch).
+      const bool lazy_first = S.lazy && first_bu;
+      const uint32_t* snap = nullptr;
+      if (lazy_first) {
+        MSBFS_HIP_CHECK(hipMemcpyAsync(asnap_.p, anyvis_.p, anyvis_.bytes, hipMemcpyDeviceToDevice, s));
+        snap = asnap_.as<uint32_t>();
+      }
+      const bool filter = lazy_first || (double)S.ev < filter_frac_ * (double)g_.nnz;
       // hub rows (lowest ids after degree relabelling) sized to ~hub_bytes_ are always loaded
       const int64_t hub_ids = g_.old2new && !S.lazy ? (int64_t)(hub_bytes_ / (8.0 * W)) : 0;
       const int32_t filter_from =
@@ -2482,7 +2517,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
                                next_wide, slabF(rows), acc_[S.ac].as<uint64_t>(),
-                               stamp_.as<int32_t>(), epoch_, plen, nullptr);
+                               stamp_.as<int32_t>(), epoch_, plen, nullptr, snap);
           if (fuse) rows += gn;
         } else if (hub_lds && (hub_lds_ & 2)) {
           constexpr int BT = 1024;
@@ -2498,7 +2533,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                               next_wide, slabF(rows), nullptr, nullptr, 0, nullptr, nullptr);
+                               next_wide, slabF(rows), nullptr, nullptr, 0, nullptr, nullptr, snap);
           if (fuse) rows += gn;
         } else {
           const int gn = grid_for(S.nact, L::TILE, grid);
@@ -2522,7 +2557,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                 touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
                 done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
                 ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                next_wide, slabF(rows), nullptr, nullptr, 0, nullptr, &ctr_.as<Ctr>()->touched.v);
+                next_wide, slabF(rows), nullptr, nullptr, 0, nullptr, &ctr_.as<Ctr>()->touched.v,
+                nullptr);
             MSBFS_HIP_CHECK(hipGetLastError());
             rows += gn;
           } else {
@@ -2535,7 +2571,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
                                    sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                    fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                    anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                                   next_wide, slabF(rows), nullptr, nullptr, 0, nullptr, nullptr);
+                                   next_wide, slabF(rows), nullptr, nullptr, 0, nullptr, nullptr, snap);
           if (fuse) rows += gn;
           }
         }
@@ -2607,13 +2643,13 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
               desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
               sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-              coop, xmode_, codes, code_from);
+              coop, xmode_, codes, code_from, snap);
         } else {
           auto ck = tile_ >= 1024 ? k_bu_chunks<W, 1024, kBlock, 0>
                     : tile_ >= 512 ? k_bu_chunks<W, 512, kBlock, 0> : k_bu_chunks<W, 256, kBlock, 0>;
           ck<<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
               desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(),
-              anyvis_.as<uint32_t>(), filter_from, coop, xmode_, codes, code_from);
+              anyvis_.as<uint32_t>(), filter_from, coop, xmode_, codes, code_from, snap);
         }
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(S.nactw, L::TILE, grid);
@@ -2622,7 +2658,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
             actw_[0].as<int32_t>(), S.nactw, g_.rowptr, R, O, acc_[S.ac].as<uint64_t>(), alive,
             sm.gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
             ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), act_[1].as<int32_t>(), next_wide,
-            slabF(rows));
+            slabF(rows), snap);
         MSBFS_HIP_CHECK(hipGetLastError());
         if (fuse) rows += gw;
       }
@@ -2639,6 +2675,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       std::swap(actw_[0], actw_[1]);
       S.cur ^= 1;
       S.fsrc_acc = false;
+      S.osnap_next = lazy_first;
       if (st) st->bu_levels++;
     }
     if (rows) {
@@ -2722,19 +2759,21 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
       k_td_expand_small<W, false><<<grid, kBlock, 0, s>>>(
           fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v, g_.rowptr, g_.col, R,
           acc_[S.ac].as<uint64_t>(), done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(),
-          stamp_.as<int32_t>(), epoch_, touched_.as<int32_t>(), cur);
+          stamp_.as<int32_t>(), epoch_, touched_.as<int32_t>(), cur,
+          S.lazy ? anyvis_.as<uint32_t>() : nullptr);
     else
       k_td_expand_small<W, true><<<grid, kBlock, 0, s>>>(
           fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v, g_.rowptr, g_.col, R, O,
           done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
-          touched_.as<int32_t>(), cur);
+          touched_.as<int32_t>(), cur, S.lazy ? anyvis_.as<uint32_t>() : nullptr,
+          S.osnap_next ? asnap_.as<uint32_t>() : nullptr);
     auto kf = fuse ? k_td_finalize<W, COUNT, FUSE> : k_td_finalize<W, COUNT, false>;
     kf<<<grid, kBlock, 0, s>>>(touched_.as<int32_t>(), g_.rowptr, R, O,
                                acc_[S.ac ^ 1].as<uint64_t>(), aslot + 16 * i, sm.gmask,
                                done_.as<uint32_t>(), fl_[S.fc ^ 1].as<int32_t>(), cur,
                                fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v,
                                S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr,
-                               anyvis_.as<uint32_t>(), slabF_.as<uint32_t>(), 0);
+                               anyvis_.as<uint32_t>(), slabF_.as<uint32_t>(), S.lazy ? 1 : 0);
     if (!fuse)
       k_count_frontier<W, COUNT, false><<<grid, kBlock, 0, s>>>(
           fl_[S.fc ^ 1].as<int32_t>(), cur, g_.rowptr, acc_[S.ac ^ 1].as<uint64_t>(), nullptr,
@@ -2748,6 +2787,7 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
     S.fc ^= 1;
     S.ac ^= 1;
     S.fsrc_acc = true;
+    S.osnap_next = false;
   }
   // alive after the batch -> the host loop's current alive buffer
   MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[S.alv], aslot + 16 * K, 16 * sizeof(uint64_t),
@@ -2798,6 +2838,9 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
                               int64_t* Fout, int64_t* edges2, RunStats* st, hipStream_t s) {
   Loop S;
   S.cnt = n_eff();
+  // lazy: no per-batch fill of vis_[0] (n_eff * 8W bytes, ~0.8 ms on RMAT-26); the edge-counting
+  // pass re-reads both rows of every new vertex (k_count_frontier), so it keeps the fill
+  S.lazy = lazy_ && !COUNT && fuse_count_ && !xcd_;
   start_batch<W, COUNT>(k0, nb, qoff, qids, S, s);
   levels<W, COUNT>(S, st, s);
   // frontier is empty: accumulator entries were cleared by finalize / zero_acc
