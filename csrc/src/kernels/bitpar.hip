@@ -534,9 +534,10 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ LdsQueue q;
   __shared__ unsigned long long scratch[kWaves];
-  __shared__ uint32_t cnt[FUSE ? 64 * W : 1];
+  constexpr int CR = 65;  // bank-skewed counter rows (see BitCounter::spill_strided)
+  __shared__ uint32_t cnt[FUSE ? CR * W : 1];
   if constexpr (FUSE)
-    for (int i = threadIdx.x; i < 64 * W; i += kBlock) cnt[i] = 0;
+    for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
   q_init(q);
   __syncthreads();
   BitCounter<VW> bc;
@@ -582,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
     if constexpr (FUSE) {  // nw is zero for invalid lanes
       bc.add(nw);
       if (++nadd == (1 << BitCounter<VW>::D) - 1) {
-        bc.spill(cnt, slot);
+        bc.template spill_strided<CR>(cnt, slot);
         nadd = 0;
       }
     }
@@ -605,10 +606,10 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
   if constexpr (FUSE) {
-    bc.spill(cnt, slot);
+    bc.template spill_strided<CR>(cnt, slot);
     __syncthreads();
     uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
-    for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i];
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
   }
   // zero the consumed top-down frontier bits of the previous frontier
   if (accCur_zero) {
@@ -1591,9 +1592,12 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   __shared__ LdsQueue qa, qf, qn;
   __shared__ unsigned long long scratch[kWaves];
-  __shared__ uint32_t cnt[FUSE ? 64 * W : 1];
+  // bank-skewed counter rows (see BitCounter::spill_strided): wide vertices gain many groups
+  // at once, so every spill touches most counters
+  constexpr int CR = 65;
+  __shared__ uint32_t cnt[FUSE ? CR * W : 1];
   if constexpr (FUSE)
-    for (int i = threadIdx.x; i < 64 * W; i += kBlock) cnt[i] = 0;
+    for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
   q_init(qa);
   q_init(qf);
   q_init(qn);
@@ -1636,7 +1640,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     if constexpr (FUSE) {  // nwb is zero for invalid lanes
       bc.add(nwb);
       if (++nadd == (1 << BitCounter<VW>::D) - 1) {
-        bc.spill(cnt, slot);
+        bc.template spill_strided<CR>(cnt, slot);
         nadd = 0;
       }
     }
@@ -1669,10 +1673,10 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
   if constexpr (FUSE) {
-    bc.spill(cnt, slot);
+    bc.template spill_strided<CR>(cnt, slot);
     __syncthreads();
     uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
-    for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i];
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
   }
 }
 
@@ -1936,6 +1940,7 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_XCD")) xcd_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
     if (const char* x = getenv("MSBFS_LEAN")) lean_ = atoi(x);
+
     if (const char* x = getenv("MSBFS_HUBBIG")) hub_big_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX")) pfx_ = atoi(x);
     if (const char* x = getenv("MSBFS_NARROW_C")) narrow_c_ = atoi(x);
