@@ -826,8 +826,8 @@ __global__ __launch_bounds__(kBlock) void k_push_tail(
 // C1 > 0 (unfiltered levels only): a first step of just C1 rows before the CS-wide steps; late
 // levels are mostly covered by the first neighbour or two (sorted rows: hubs first).
 template <int W, bool COUNT, int BT, int HUBW, bool FUSE, bool FILT = true, bool PFX = false,
-          int CS = 8, int C1 = 0>
-__global__ __launch_bounds__(BT, 4) void k_bu_narrow(
+          int CS = 8, int C1 = 0, int MINW = 4>
+__global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
@@ -2513,7 +2513,9 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         if (pfx) {
           constexpr int BT = 1024;
           const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
-          auto kn = fuse ? (pfx_small ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE, true, true>
+          // 4-neighbour steps: 122 VGPRs, no spills (8-neighbour steps spilled at the 128-VGPR
+          // bound): RMAT-26 5.17 -> 4.96 ms (the full pulls of level 3 keep 8: 5.8 vs 6.8 ms)
+          auto kn = fuse ? (pfx_small ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE, true, true, 4>
                                       : k_bu_narrow<W, COUNT, BT, kHubBig, FUSE, true, true>)
                          : (pfx_small ? k_bu_narrow<W, COUNT, BT, kHubW, false, true, true>
                                       : k_bu_narrow<W, COUNT, BT, kHubBig, false, true, true>);
