@@ -1187,7 +1187,7 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
                                            const uint64_t* R, const V<Lay<W>::VW>& am,
                                            uint64_t* acc, const uint32_t* anyvis,
                                            const uint32_t* hub, int32_t filter_from, int coop,
-                                           int xmode, int32_t* lst, const uint32_t* code,
+                                           int32_t* lst, const uint32_t* code,
                                            int32_t code_from, unsigned long long* wacc,
                                            const uint32_t* snap) {
   using L = Lay<W>;
@@ -1227,7 +1227,7 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
       const int64_t e = t0 + q * 64 + lane;
       u[q] = e < lim ? col[e] : -1;
     }
-    if (!(xmode & 2) && filter_from != INT32_MAX) {
+    if (filter_from != INT32_MAX) {
       // probes: every load first, every use after (see k_bu_narrow)
       uint32_t pg[Q], ph[Q];  // separate destinations (see k_bu_narrow)
 #pragma unroll
@@ -1285,7 +1285,7 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
         const int k = b + q * S + sub;
         uu[q] = k < cnt ? lst[k] : -1;
       }
-      if (!(xmode & 1)) {
+      {
         // loads first, ORs after: the compiler then keeps all PB loads in flight
         V<VW> x[PB];
 #pragma unroll
@@ -1400,7 +1400,7 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const ChunkDesc* __restrict__ desc, const int64_t* nchunks_p, const int32_t* col,
     const uint64_t* R,
     const uint64_t* alive, const uint64_t* gmask, uint64_t* acc, const uint32_t* anyvis,
-    int32_t filter_from, int coop, int xmode, const uint32_t* code, int32_t code_from,
+    int32_t filter_from, int coop, const uint32_t* code, int32_t code_from,
     const uint32_t* snap) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G;
@@ -1434,150 +1434,8 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const int64_t beg = uni64((int64_t)(((uint64_t)d.beg_hi << 32) | d.beg_lo));
     const int64_t lim = beg + uni32(d.len);
     if (c + cstep < cend) d = desc[c + cstep];  // next descriptor, in flight during the pull
-    chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop, xmode,
+    chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop,
                            lst, code, code_from, wacc[threadIdx.x >> 6], snap);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// XCD-labelled chunks (first bottom-up level). There every unvisited vertex scans its whole row
-// and gathers the 8*W-byte visited row of every level-1-frontier neighbour; those rows (tens of
-// MB at W = 16) do not fit one XCD's 4 MB L2, so most gathers went to the Infinity Cache. Here
-// the neighbour-id space is cut into kLabels ranges and each wide vertex's (sorted) row into
-// the matching segments; segment chunks of range x go to blocks with blockIdx % 8 == x, which
-// share an XCD under the observed round-robin dispatch, so each XCD's L2 holds only its range's
-// rows. Placement is a speed hint only: any block may run any chunk (waves steal from the other
-// ranges' queues once their own is empty), so correctness never depends on it.
-// seg[x*nw + i] = first column position of range x in wide vertex i's row (x = 0..kLabels).
-// ---------------------------------------------------------------------------------------------
-constexpr int kLabels = 8;
-struct LabelBounds {
-  int32_t b[kLabels + 1];  // neighbour id ranges [b[x], b[x+1])
-};
-
-__global__ __launch_bounds__(kBlock) void k_seg_split(const int32_t* wl, int64_t nw,
-                                                      const int64_t* rowptr, const int32_t* col,
-                                                      LabelBounds lb, int64_t* seg) {
-  const int64_t total = nw * (kLabels + 1);
-  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * kBlock) {
-    const int64_t i = t % nw;
-    const int x = (int)(t / nw);
-    const int32_t v = wl[i];
-    int64_t lo = rowptr[v], hi = rowptr[v + 1];
-    if (x == 0) {
-      seg[i] = lo;
-    } else if (x == kLabels) {
-      seg[(int64_t)kLabels * nw + i] = hi;
-    } else {
-      const int32_t key = lb.b[x];
-      while (lo < hi) {  // first position with col >= key (rows are sorted)
-        const int64_t mid = (lo + hi) >> 1;
-        if (col[mid] < key) lo = mid + 1;
-        else hi = mid;
-      }
-      seg[(int64_t)x * nw + i] = lo;
-    }
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_seg_counts(const int64_t* seg, int64_t nw,
-                                                       int64_t* cnt) {
-  const int64_t total = nw * kLabels;
-  for (int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x; f < total;
-       f += (int64_t)gridDim.x * kBlock) {
-    const int64_t len = max(seg[f + nw] - seg[f], (int64_t)0);  // (sorted rows: never < 0)
-    cnt[f] = (len + kChunk - 1) / kChunk;
-  }
-}
-
-// owner[c] = f (= x*nw + i) for every chunk c of segment f (P = inclusive chunk-count prefix)
-__global__ __launch_bounds__(kBlock) void k_seg_owner(const int64_t* P, int64_t nf,
-                                                      int32_t* owner) {
-  for (int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x; f < nf;
-       f += (int64_t)gridDim.x * kBlock) {
-    const int64_t e = P[f];
-    for (int64_t c = f ? P[f - 1] : 0; c < e; ++c) owner[c] = (int32_t)f;
-  }
-}
-
-// b[x] = first vertex v with rowptr[v] >= x/kLabels of the edge endpoints (equal endpoint mass
-// per range: after degree relabelling range 0 is a few hundred hubs, the last one the tail)
-__global__ void k_label_bounds(const int64_t* rowptr, int64_t n, int32_t* b) {
-  const int x = (int)threadIdx.x;
-  if (x > kLabels) return;
-  const int64_t total = rowptr[n];
-  const int64_t target = total / kLabels * x + total % kLabels * x / kLabels;
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (rowptr[mid] >= target) hi = mid;
-    else lo = mid + 1;
-  }
-  b[x] = x == 0 ? 0 : (x == kLabels ? (int32_t)n : (int32_t)lo);
-}
-
-struct alignas(128) QHead {
-  unsigned long long v;
-  uint32_t pad[30];
-};
-
-template <int W, int T, int BT, int HUBW>
-__global__ __launch_bounds__(BT) void k_bu_chunks_xcd(
-    const int32_t* wl, int64_t nw, const int64_t* seg, const int64_t* P, const int32_t* owner,
-    const int32_t* col, const uint64_t* R, const uint64_t* alive, const uint64_t* gmask,
-    uint64_t* acc, const uint32_t* anyvis, int32_t filter_from, int xmode, QHead* heads) {
-  using L = Lay<W>;
-  constexpr int VW = L::VW, G = L::G;
-  constexpr int BATCH = 2;  // chunks per dequeue
-  __shared__ int32_t tile[BT / 64][T];
-  __shared__ unsigned long long wacc[BT / 64][W];
-  __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
-  if constexpr (HUBW > 0) {
-    for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
-    __syncthreads();
-  }
-  const int lane = lane_id(), slot = lane % G;
-  int32_t* lst = tile[threadIdx.x >> 6];
-  V<VW> am;
-#pragma unroll
-  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  const int x0 = (int)(blockIdx.x % kLabels);
-  for (int k = 0; k < kLabels; ++k) {  // own range first, then steal
-    const int x = (x0 + k) % kLabels;
-    // Every value steering the loops is made wave-uniform (uni*): with a __shfl broadcast of
-    // the dequeued index the loops compiled as exec-masked "divergent" loops, and ROCm 7.2 turned
-    // the W <= 2 instantiations into loops that never ended.
-    const int64_t cbeg = x ? uni64(P[(int64_t)x * nw - 1]) : 0;
-    const int64_t ncx = uni64(P[(int64_t)(x + 1) * nw - 1]) - cbeg;
-    while (true) {
-      unsigned long long r = 0;
-      if (lane == 0) r = atomicAdd(&heads[x].v, (unsigned long long)BATCH);
-      const int64_t c0 = uni64((int64_t)r);
-      if (c0 >= ncx) break;
-      for (int q = 0; q < BATCH; ++q) {
-        const int64_t c = c0 + q;
-        if (c >= ncx) break;
-        const int64_t f = uni32(owner[cbeg + c]);
-        const int64_t i = f - (int64_t)x * nw;
-        const int32_t v = uni32(wl[i]);
-        const int64_t j0 = cbeg + c - (f ? uni64(P[f - 1]) : 0);
-        const int64_t beg = uni64(seg[f]) + j0 * kChunk;
-        const int64_t lim = min(uni64(seg[f + nw]), beg + (int64_t)kChunk);
-        chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, 0, xmode,
-                               lst, nullptr, kNoCodes, wacc[threadIdx.x >> 6], nullptr);
-      }
-    }
-  }
-}
-
-// owner[c] = i for every chunk c of wide-list entry i (offs = inclusive chunk-count prefix)
-__global__ __launch_bounds__(kBlock) void k_chunk_owner(const int64_t* offs, int64_t nw,
-                                                        int32_t* owner) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
-       i += (int64_t)gridDim.x * kBlock) {
-    const int64_t e = offs[i];
-    for (int64_t c = i ? offs[i - 1] : 0; c < e; ++c) owner[c] = (int32_t)i;
   }
 }
 
@@ -1920,7 +1778,6 @@ class BitparSolver final : public Solver {
       fl_[i].alloc((size_t)n * sizeof(int32_t));
     }
     touched_.alloc((size_t)n * sizeof(int32_t));
-    owner_.alloc(((size_t)n + (size_t)(g.nnz / kChunk) + 2) * sizeof(int32_t));  // >= chunks_max
     offs_.alloc((size_t)n * sizeof(int64_t));
     scan_bytes_ = frontier_scan_temp_bytes(n);
     scan_tmp_.alloc(scan_bytes_);
@@ -1933,11 +1790,9 @@ class BitparSolver final : public Solver {
     hsmall_ = std::make_unique<PinnedBuf>(small_.bytes);
     if (const char* d = getenv("MSBFS_DIRS")) dirs_ = d;  // per-level T/B override (tuning)
     if (const char* w = getenv("MSBFS_WIDE_LATER")) wide_later_ = atoi(w);
-    if (const char* x = getenv("MSBFS_X")) xmode_ = atoi(x);          // experiments only
     if (const char* t = getenv("MSBFS_TILE")) tile_ = atoi(t);
     if (const char* h = getenv("MSBFS_HUBLDS")) hub_lds_ = atoi(h);
     if (const char* f = getenv("MSBFS_FUSE_COUNT")) fuse_count_ = atoi(f);
-    if (const char* x = getenv("MSBFS_XCD")) xcd_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
     if (const char* x = getenv("MSBFS_LEAN")) lean_ = atoi(x);
 
@@ -1953,7 +1808,6 @@ class BitparSolver final : public Solver {
     if (const char* b = getenv("MSBFS_BATCH")) batch_levels_ = std::max(1, std::min(kBatch, atoi(b)));
     bctr_.alloc((size_t)(kBatch + 1) * (sizeof(Ctr) + 16 * sizeof(uint64_t)));
     hbctr_ = std::make_unique<PinnedBuf>((size_t)(kBatch + 1) * sizeof(Ctr));
-    heads_.alloc(sizeof(QHead) * kLabels);
     MSBFS_HIP_CHECK(hipDeviceSynchronize());
   }
 
@@ -2106,18 +1960,6 @@ class BitparSolver final : public Solver {
 #undef MSBFS_BP_CASE
   }
 
-  LabelBounds label_bounds() {
-    if (lb_key_[0] != (const void*)g_.rowptr || lb_key_[1] != (const void*)g_.col) {
-      DevBuf d;
-      d.alloc(sizeof(int32_t) * (kLabels + 1));
-      k_label_bounds<<<1, 64>>>(g_.rowptr, n_eff(), d.as<int32_t>());
-      MSBFS_HIP_CHECK(hipGetLastError());
-      MSBFS_HIP_CHECK(hipMemcpy(lb_.b, d.p, sizeof(lb_.b), hipMemcpyDeviceToHost));
-      lb_key_[0] = g_.rowptr;
-      lb_key_[1] = g_.col;
-    }
-    return lb_;
-  }
 
   // 1 + the last vertex with deg > 0 (cached per graph buffers: relabelling replaces them).
   // Vertices beyond it are never active, never neighbours: level loops and clears skip them.
@@ -2164,7 +2006,7 @@ class BitparSolver final : public Solver {
   const DeviceGraph& g_;
   int maxW_ = 1;
   DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
-      ctr_, small_, pairs_, slabF_, slabE_, anyvis_, owner_, desc_;
+      ctr_, small_, pairs_, slabF_, slabE_, anyvis_, desc_;
   double filter_frac_ = 0.5;  // skip unvisited neighbours while visited edges < frac * nnz
   double hub_bytes_ = 0.0;    // MSBFS_HUB_MB: hub rows loaded without the bitmap test (off: best)
   size_t scan_bytes_ = 0;
@@ -2172,19 +2014,11 @@ class BitparSolver final : public Solver {
   int32_t epoch_ = 0;
   std::string dirs_;
   int wide_later_ = 1024;
-  int xmode_ = 0;
   int tile_ = 256;
   int hub_lds_ = 3;  // bit 0: chunks kernel, bit 1: narrow kernel (MSBFS_HUBLDS)
   int fuse_count_ = 1;  // MSBFS_FUSE_COUNT=0: separate k_count_frontier pass
   int64_t n_eff_ = 0;
   const void* eff_key_[3] = {nullptr, nullptr, nullptr};
-  LabelBounds lb_{};
-  const void* lb_key_[2] = {nullptr, nullptr};
-  DevBuf segb_, segc_, segt_, heads_;
-  // MSBFS_XCD=1: first bottom-up level through XCD-labelled segments. Off: measured 2.7x slower
-  // on RMAT-26 (24.4 -> 65.6 ms for level 2) because cutting every wide row into 8 neighbour
-  // ranges multiplies the per-chunk overhead and the dequeue atomics (16M segments at wd = 32).
-  int xcd_ = 0;
   // sparse row codes on the first bottom-up level (MSBFS_CODES=0: off); ids with degree >=
   // code_deg_ * nnz / (source degree sum), i.e. expected >= code_deg_ set bits, keep row gathers
   int codes_ = 1;
@@ -2604,45 +2438,12 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
         // most of every hub's groups already visited) the early exit skips most chunks.
         // MSBFS_COOP: 1 always, 0 = never on the first bottom-up level (the old rule).
         const int coop = !first_bu ? 1 : coop_ == 1 ? 1 : coop_ == 0 ? 0 : (S.level == 2 ? 0 : 1);
-        const bool use_xcd =
-            !pfx && first_bu && xcd_ && g_.rows_sorted && S.nactw >= 1024 && n <= INT32_MAX;
-        if (!use_xcd) {
-          desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
-          k_chunk_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
-              actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, plen,
-              desc_.as<ChunkDesc>());
-          MSBFS_HIP_CHECK(hipGetLastError());
-        }
-        if (use_xcd) {
-          // first bottom-up level: XCD-labelled segment chunks (see k_bu_chunks_xcd)
-          const LabelBounds lb = label_bounds();
-          const int64_t nw = S.nactw, nf = (int64_t)kLabels * nw;
-          segb_.ensure((size_t)(nf + nw) * sizeof(int64_t));
-          segc_.ensure((size_t)nf * sizeof(int64_t) * 2);
-          const size_t tb = inclusive_scan_temp_bytes(nf);
-          segt_.ensure(tb);
-          owner_.ensure((size_t)(nf + S.ea / kChunk + kLabels + 1) * sizeof(int32_t));
-          int64_t* seg = segb_.as<int64_t>();
-          int64_t* cnt = segc_.as<int64_t>();
-          int64_t* P = cnt + nf;
-          k_seg_split<<<grid_for(nf + nw, kBlock, 8192), kBlock, 0, s>>>(
-              actw_[0].as<int32_t>(), nw, g_.rowptr, g_.col, lb, seg);
-          k_seg_counts<<<grid_for(nf, kBlock, 8192), kBlock, 0, s>>>(seg, nw, cnt);
-          inclusive_scan_i64(cnt, P, nf, segt_.p, segt_.bytes, s);
-          k_seg_owner<<<grid_for(nf, kBlock, 8192), kBlock, 0, s>>>(P, nf, owner_.as<int32_t>());
-          MSBFS_HIP_CHECK(hipMemsetAsync(heads_.p, 0, heads_.bytes, s));
-          MSBFS_HIP_CHECK(hipGetLastError());
-          if (hub_lds && (hub_lds_ & 1))
-            k_bu_chunks_xcd<W, 256, 1024, kHubW><<<512, 1024, 0, s>>>(
-                actw_[0].as<int32_t>(), nw, seg, P, owner_.as<int32_t>(), g_.col, R, alive,
-                sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, xmode_,
-                heads_.as<QHead>());
-          else
-            k_bu_chunks_xcd<W, 256, 1024, 0><<<512, 1024, 0, s>>>(
-                actw_[0].as<int32_t>(), nw, seg, P, owner_.as<int32_t>(), g_.col, R, alive,
-                sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, xmode_,
-                heads_.as<QHead>());
-        } else if (hub_lds && (hub_lds_ & 1)) {
+        desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
+        k_chunk_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
+            actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, plen,
+            desc_.as<ChunkDesc>());
+        MSBFS_HIP_CHECK(hipGetLastError());
+        if (hub_lds && (hub_lds_ & 1)) {
           // exact chunk count = offs[nactw - 1], read on the device (no host round trip)
           // MSBFS_HUBBIG bit 1: one block per CU with a 128-KB hub bitmap (ids < 1M)
           const bool big = (hub_big_ & 2) && n > (int64_t)kHubBig * 32 * 4 && !(pfx && pfx_small);
@@ -2650,13 +2451,13 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
               desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
               sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-              coop, xmode_, codes, code_from, snap);
+              coop, codes, code_from, snap);
         } else {
           auto ck = tile_ >= 1024 ? k_bu_chunks<W, 1024, kBlock, 0>
                     : tile_ >= 512 ? k_bu_chunks<W, 512, kBlock, 0> : k_bu_chunks<W, 256, kBlock, 0>;
           ck<<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
               desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(),
-              anyvis_.as<uint32_t>(), filter_from, coop, xmode_, codes, code_from, snap);
+              anyvis_.as<uint32_t>(), filter_from, coop, codes, code_from, snap);
         }
         MSBFS_HIP_CHECK(hipGetLastError());
         const int gw = grid_for(S.nactw, L::TILE, grid);
@@ -2847,7 +2648,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
   S.cnt = n_eff();
   // lazy: no per-batch fill of vis_[0] (n_eff * 8W bytes, ~0.8 ms on RMAT-26); the edge-counting
   // pass re-reads both rows of every new vertex (k_count_frontier), so it keeps the fill
-  S.lazy = lazy_ && !COUNT && fuse_count_ && !xcd_;
+  S.lazy = lazy_ && !COUNT && fuse_count_;
   start_batch<W, COUNT>(k0, nb, qoff, qids, S, s);
   levels<W, COUNT>(S, st, s);
   // frontier is empty: accumulator entries were cleared by finalize / zero_acc

@@ -84,7 +84,6 @@ for s in "$@"; do
          step pmcn2 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_VALU --kernel-include-regex "k_bu_narrow" --output-format csv -d gpurun_out/pmcn2 -o run -- python bench.py --steps 1 --warmup 0 --groups 128
          step pmcn3 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum --kernel-include-regex "k_bu_narrow" --output-format csv -d gpurun_out/pmcn3 -o run -- python bench.py --steps 1 --warmup 0 --groups 128
          ;;
-    xexp) for x in 1 2 3; do MSBFS_X=$x MSBFS_TRACE=1 step xexp$x 300 python bench.py --steps 1 --warmup 0; done ;;
     t26) MSBFS_TRACE=1 step t26 300 python bench.py --steps 2 --warmup 1 ;;
     pmcbu) export TMPDIR=/tmp; R="k_bu_chunks|k_bu_narrow"
          step pmcb1 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmcb1 -o run -- python bench.py --steps 1 --warmup 0
