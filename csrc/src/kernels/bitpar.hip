@@ -1905,6 +1905,8 @@ class BitparSolver final : public Solver {
     int64_t ef0 = 0;                    // degree sum of the sources (level-0 frontier)
     bool lazy = false;                  // no vis_[0] fill (see start_batch)
     bool osnap_next = false;            // the previous level was the first pull of a lazy batch
+    bool lean_off = false;              // a lean first-row pass overflowed (see k_bu_first)
+    bool lean_ran = false;              // this level ran one (its overflow count is c.touched)
   };
   struct Small {
     unsigned long long* F;
@@ -2385,7 +2387,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           // 4 3.1 -> 2.5 ms; level 3 prefers full steps: 6.5 vs 6.7 ms). MSBFS_NARROW_C: 0 off,
           // 1 always, 2 (default) this rule
           const bool short1 = narrow_c_ == 1 || (narrow_c_ == 2 && (S.bu_levels >= 3 || W <= 4));
-          if (lean_ && fuse && !filt && S.bu_levels >= 3 && S.nact >= (1 << 20)) {
+          if (lean_ && !S.lean_off && fuse && !filt && S.bu_levels >= 3 && S.nact >= (1 << 20)) {
+            S.lean_ran = true;
             // lean first pass, then the regular pull over the vertices it could not finish
             const int gl = grid_for(S.nact, L::TILE, grid);
             k_bu_first<W><<<gl, kBlock, 0, s>>>(
@@ -2494,6 +2497,12 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       MSBFS_HIP_CHECK(hipGetLastError());
     }
     c = read_ctr(s);
+    if (S.lean_ran) {
+      // (high-diameter graphs: most vertices need more than their first neighbour; once a lean
+      // pass sends over a quarter of its vertices on, the batch keeps the regular pull)
+      if ((int64_t)c.touched * 4 > S.nact) S.lean_off = true;
+      S.lean_ran = false;
+    }
     if (bottom_up) {
       S.nact = c.act2;
       S.nactw = c.actw2;
