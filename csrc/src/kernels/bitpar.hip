@@ -1795,6 +1795,7 @@ class BitparSolver final : public Solver {
     if (const char* f = getenv("MSBFS_FUSE_COUNT")) fuse_count_ = atoi(f);
     if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
     if (const char* x = getenv("MSBFS_LEAN")) lean_ = atoi(x);
+    if (const char* x = getenv("MSBFS_LEAN_MIN")) lean_min_ = atoll(x);
 
     if (const char* x = getenv("MSBFS_HUBBIG")) hub_big_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX")) pfx_ = atoi(x);
@@ -2028,6 +2029,7 @@ class BitparSolver final : public Solver {
   // RMAT-26, 1024 groups: level 4 2.48 -> 2.07 ms (98 % of its vertices finish on the first
   // row); on the second pull level most vertices overflow (128 groups: level 3 3.5 -> 4.1 ms)
   int lean_ = 1;
+  int64_t lean_min_ = 1 << 20;  // MSBFS_LEAN_MIN: smallest active list for the lean pass
   DevBuf plen_;
   const void* plen_key_[2] = {nullptr, nullptr};
   int32_t plen_h_ = 0;
@@ -2387,7 +2389,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           // 4 3.1 -> 2.5 ms; level 3 prefers full steps: 6.5 vs 6.7 ms). MSBFS_NARROW_C: 0 off,
           // 1 always, 2 (default) this rule
           const bool short1 = narrow_c_ == 1 || (narrow_c_ == 2 && (S.bu_levels >= 3 || W <= 4));
-          if (lean_ && !S.lean_off && fuse && !filt && S.bu_levels >= 3 && S.nact >= (1 << 20)) {
+          if (lean_ && !S.lean_off && fuse && !filt && S.bu_levels >= 3 && S.nact >= lean_min_) {
             S.lean_ran = true;
             // lean first pass, then the regular pull over the vertices it could not finish
             const int gl = grid_for(S.nact, L::TILE, grid);

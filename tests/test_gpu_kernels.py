@@ -273,3 +273,28 @@ def test_bitpar_forced_direction_plans(msbfs_pkg, monkeypatch, dirs):
             r2 = s.run(qs)
         assert np.array_equal(r.F, ref.F), (dirs, K)
         assert np.array_equal(r2.F, ref.F), (dirs, K)
+
+
+@pytest.mark.parametrize("knobs", [{"MSBFS_LEAN_MIN": "0"}, {"MSBFS_LEAN": "0"},
+                                   {"MSBFS_LAZY": "0"}, {"MSBFS_LAZY": "0", "MSBFS_LEAN_MIN": "0"}])
+def test_bitpar_lean_and_lazy_paths(msbfs_pkg, monkeypatch, knobs):
+    """The lean first-row pass on late pull levels (k_bu_first + overflow pull; forced on small
+    lists with MSBFS_LEAN_MIN=0) and the lazy batches without the visited-buffer fill agree with
+    the CPU oracle, with each switched on and off, over several batches and a reused solver."""
+    m = msbfs_pkg
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    dg = m.DeviceGraph.rmat(15, 16, 7, device=0)
+    hg = dg.download()
+    dg.relabel_by_degree()
+    cases = [(dg, hg, 1024), (dg, hg, 2100), (dg, hg, 128)]
+    for name, g in _graphs(m)[2:4]:
+        cases.append((g.to_device(0), g, 300))
+    for dev, host, K in cases:
+        qs = m.QuerySet.random(host.n, K, 8, seed=K + 1)
+        ref = m.cpu_bfs(host, qs)
+        with m.Solver(dev, "bitpar", max_groups=min(K, 1024)) as s:
+            r = s.run(qs)
+            r2 = s.run(qs)
+        assert np.array_equal(r.F, ref.F), (knobs, K)
+        assert np.array_equal(r2.F, ref.F), (knobs, K)
