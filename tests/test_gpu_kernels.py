@@ -298,3 +298,52 @@ def test_bitpar_lean_and_lazy_paths(msbfs_pkg, monkeypatch, knobs):
             r2 = s.run(qs)
         assert np.array_equal(r.F, ref.F), (knobs, K)
         assert np.array_equal(r2.F, ref.F), (knobs, K)
+
+
+def _hyp_strategy():
+    from hypothesis import strategies as st
+
+    @st.composite
+    def graphs_and_queries(draw):
+        n = draw(st.integers(1, 60))
+        m_ = draw(st.integers(0, 150))
+        edges = draw(st.lists(st.tuples(st.integers(0, n - 1), st.integers(0, n - 1)),
+                              min_size=m_, max_size=m_))
+        K = draw(st.integers(1, 140))  # up to three 64-group words
+        groups = draw(st.lists(st.lists(st.integers(-3, n + 3), max_size=6), min_size=K,
+                               max_size=K))
+        return n, edges, groups
+    return graphs_and_queries()
+
+
+def test_device_algos_property(msbfs_pkg):
+    """SURVEY §4.2 item 3 on the GPU: hypothesis-generated graphs (self-loops, duplicate edges,
+    isolated vertices) and query sets (empty groups, out-of-range ids) through every device
+    algorithm, against the CPU path and the numpy oracle of the reference semantics."""
+    from hypothesis import given, settings, HealthCheck
+    from msbfs.ops import reference as R
+    m = msbfs_pkg
+
+    @settings(max_examples=60, deadline=None, suppress_health_check=list(HealthCheck))
+    @given(_hyp_strategy())
+    def check(data):
+        n, edges, groups = data
+        u = np.array([e[0] for e in edges], np.int32)
+        v = np.array([e[1] for e in edges], np.int32)
+        g = m.Graph.from_edges(n, u, v)
+        qs = m.QuerySet.from_groups(groups)
+        ref = m.cpu_bfs(g, qs, count_edges=True)
+        for k in range(min(qs.K, 5)):
+            assert ref.F[k] == R.bfs_F_numpy(g.n, g.rowptr, g.col, qs.group(k))[0]
+        dg = g.to_device(0)
+        for algo in ("bitpar", "dist", "topdown", "sweep"):
+            sub = qs if algo == "bitpar" else qs.subset(np.arange(min(qs.K, 6)))
+            with m.Solver(dg, algo, max_groups=sub.K) as s:
+                r = s.run(sub, count_edges=True)
+            assert np.array_equal(r.F, ref.F[:sub.K]), algo
+            assert np.array_equal(r.edges, ref.edges[:sub.K]), algo
+        with m.Solver(dg, "bitpar", max_groups=qs.K) as s:  # fused-count (lazy) path
+            assert np.array_equal(s.run(qs).F, ref.F)
+        dg.close()
+
+    check()
