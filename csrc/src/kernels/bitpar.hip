@@ -423,18 +423,22 @@ __global__ __launch_bounds__(kBlock) void k_td_expand(
         }
         // lzv: rows of never-visited vertices may be stale (lazy reset, see k_zero_part_rows)
         const V<VW> r = (lzv && !any_visited(lzv, v)) ? vzero<VW>() : ldv<VW>(visCur + vo);
-        bool any = false;
+        bool any = false, first = false;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
           const uint64_t mm = fb.w[j] & ~r.w[j];
           if (mm) {
-            atomicOr((unsigned long long*)&accNext[vo + j], mm);
+            first |= atomicOr((unsigned long long*)&accNext[vo + j], mm) == 0ull;
             any = true;
           }
         }
-        // one lane per group decides the first touch of v in this level (the group shares v)
-        const uint64_t gm = (__ballot(any) >> (sub * G)) & L::GBITS;
-        if (gm && slot == 0) touch = atomicExch(&stamp[v], epoch) != epoch;
+        if constexpr (W == 1) {
+          touch = first;  // (see k_td_expand_small)
+        } else {
+          // one lane per group decides the first touch of v in this level (the group shares v)
+          const uint64_t gm = (__ballot(any) >> (sub * G)) & L::GBITS;
+          if (gm && slot == 0) touch = atomicExch(&stamp[v], epoch) != epoch;
+        }
       }
     }
     q_push(q, touch, v);
@@ -492,17 +496,23 @@ __global__ __launch_bounds__(kBlock) void k_td_expand_small(
         if (!is_done(done, v)) {
           const int64_t vo = (int64_t)v * W + slot * VW;
           const V<VW> r = (lzv && !any_visited(lzv, v)) ? vzero<VW>() : ldv<VW>(visCur + vo);
-          bool any = false;
+          bool any = false, first = false;
 #pragma unroll
           for (int j = 0; j < VW; ++j) {
             const uint64_t mm = fb.w[j] & ~r.w[j];
             if (mm) {
-              atomicOr((unsigned long long*)&accNext[vo + j], mm);
+              first |= atomicOr((unsigned long long*)&accNext[vo + j], mm) == 0ull;
               any = true;
             }
           }
-          const uint64_t gm = (__ballot(any) >> (sub * G)) & L::GBITS;
-          if (gm && slot == 0) touch = atomicExch(&stamp[v], epoch) != epoch;
+          if constexpr (W == 1) {
+            // one word per vertex: the accumulator is all zero at the level start, so the push
+            // that finds it empty is v's first touch (no second atomic on the stamp)
+            touch = first;
+          } else {
+            const uint64_t gm = (__ballot(any) >> (sub * G)) & L::GBITS;
+            if (gm && slot == 0) touch = atomicExch(&stamp[v], epoch) != epoch;
+          }
         }
         ++e;
       }
