@@ -80,9 +80,11 @@ def main() -> int:
                           wide_degree=args.wide_degree, max_words=args.max_words)
     # Every rank must pick the same candidates (hybrid and round-robin call different
     # collectives), but hybrid_max_groups() depends on the free HBM each rank saw: agree on it.
+    # (the hybrid exchange moves rows by vertex id: every rank must number vertices alike)
     hybrid_local = (ctx.distributed and args.algo == "bitpar" and ctx.world <= H.MAX_PARTS
                     and 1 <= qs.K <= solver.hybrid_max_groups())
-    hybrid_ok = D.allreduce_max(0.0 if hybrid_local else 1.0, ctx) == 0.0
+    same_ids = D.allreduce_max(float(relabelled), ctx) == -D.allreduce_max(-float(relabelled), ctx)
+    hybrid_ok = D.allreduce_max(0.0 if hybrid_local else 1.0, ctx) == 0.0 and same_ids
     if args.dist == "hybrid" and not hybrid_ok:
         print("bench: hybrid mode needs >1 rank, --algo bitpar and K <= one pass", file=sys.stderr)
         return 2

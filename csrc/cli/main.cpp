@@ -10,7 +10,7 @@
 //   --gen rmat:SCALE:EF:SEED | uniform:N:M:SEED   (per-rank device generation, no broadcast)
 //   --qgen K:SIZE:SEED                            (generated query groups)
 //   --threads N (cpu algo)  --cache (CSR sidecar, off by default like the reference's re-read;
-//   --no-cache is accepted)  --json  --sort-rows  --repeat R
+//   --no-cache is accepted)  --json  --sort-rows  --no-relabel  --repeat R
 //   --dist {auto,roundrobin,hybrid}  multi-rank decomposition (auto: hybrid when > 1 rank, the
 //          bit-parallel solver and K <= one pass; see kernels/bitpar.hip "hybrid")
 #include <hip/hip_runtime.h>
@@ -39,7 +39,7 @@ struct Args {
   int numGPU = 1;
   int threads = 0;
   int repeat = 1;
-  bool cache = false, json = false, sort_rows = false;
+  bool cache = false, json = false, sort_rows = false, relabel = true;
 };
 
 std::vector<std::string> split(const std::string& s, char d) {
@@ -109,6 +109,7 @@ int main(int argc, char* argv[]) {
     else if (!strcmp(argv[i], "--no-cache")) a.cache = false;
     else if (!strcmp(argv[i], "--json")) a.json = true;
     else if (!strcmp(argv[i], "--sort-rows")) a.sort_rows = true;
+    else if (!strcmp(argv[i], "--no-relabel")) a.relabel = false;
   }
 
   std::unique_ptr<Comm> comm;  // outlives the try block: the catch may have to abort it
@@ -218,6 +219,18 @@ int main(int argc, char* argv[]) {
     }
     const int64_t nverts = cpu ? hg.n : dg.n;
     if (!cpu && a.sort_rows) device_graph_sort_rows(dg, stream);
+    // degree-descending ids (part of preprocessing, like the CSR build): the bit-parallel
+    // solver's prefix pulls and hub bitmaps rely on them; F does not depend on the numbering.
+    // Best effort (a graph without room for a second column array keeps its ids).
+    bool relabelled = false;
+    if (!cpu && a.relabel) {
+      try {
+        device_graph_relabel_by_degree(dg, stream);
+        relabelled = true;
+      } catch (const Error& e) {
+        fprintf(stderr, "msbfs: rank %d keeps the file's vertex ids: %s\n", comm->rank(), e.what());
+      }
+    }
 
     // ---- queries: one packed broadcast instead of 2K+1 (main.cu:257-280) ---------------------
     QuerySet q;
@@ -277,7 +290,10 @@ int main(int argc, char* argv[]) {
     // sharing a GPU see less): agree with a MIN all-reduce of the local eligibility.
     const bool hybrid_local = want_hybrid && K >= 1 && P <= Solver::kHybridMaxParts &&
                               K <= solver->hybrid_max_groups();
-    const bool hybrid = comm->allreduce_min_u64(hybrid_local ? 1 : 0) == 1;
+    // (the hybrid exchange moves rows by vertex id: every rank must number vertices alike)
+    const bool same_ids = comm->allreduce_min_u64(relabelled ? 1 : 0) == 1 ||
+                          comm->allreduce_min_u64(relabelled ? 0 : 1) == 1;
+    const bool hybrid = comm->allreduce_min_u64(hybrid_local ? 1 : 0) == 1 && same_ids;
     if (a.dist == "hybrid" && !hybrid && me == 0)
       fprintf(stderr,
               "msbfs: --dist hybrid needs --algo bitpar, <= %d ranks and K <= one pass on every "

@@ -38,6 +38,10 @@ def main(argv=None) -> int:
             cfg.qgen = argv[i + 1]; i += 1
         elif a == "--cache":
             cfg.use_cache = True
+        elif a == "--sort-rows":
+            cfg.sort_rows = True
+        elif a == "--no-relabel":
+            cfg.relabel = False
         elif a == "--json":
             json_out = True
             cfg.count_edges = True

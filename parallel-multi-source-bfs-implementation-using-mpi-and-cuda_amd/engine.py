@@ -33,6 +33,7 @@ class JobConfig:
     use_cache: bool = False
     count_edges: bool = False
     sort_rows: bool = False
+    relabel: bool = True            # degree-descending internal ids (best effort)
     solver_opts: dict = field(default_factory=dict)
 
 
@@ -116,6 +117,16 @@ class Engine:
                     self.dgraph = DeviceGraph.from_host(self.graph_host, ctx.device)
         if self.dgraph is not None and cfg.sort_rows:
             self.dgraph.sort_rows()
+        if self.dgraph is not None and cfg.relabel and self.on_gpu:
+            # the bit-parallel solver's prefix pulls rely on degree order; F does not depend on
+            # the numbering, and each rank solves its own groups (round robin), so a rank without
+            # room for the rebuild simply keeps the file's ids
+            from .ops import native
+            try:
+                self.dgraph.relabel_by_degree()
+            except native.MsbfsError as e:
+                import sys
+                print(f"msbfs: rank {ctx.rank} keeps the file's vertex ids: {e}", file=sys.stderr)
         self.n = self.dgraph.n if self.dgraph is not None else self.graph_host.n
         # queries
         if cfg.qgen:

@@ -104,3 +104,22 @@ def test_cli_gpu_rccl_one_rank(tmp_path, msbfs_pkg, dist):
               "--comm", "rccl", "--dist", dist, "--json"])
     js = _check(r, ref, m, 1)
     assert js["comm"] == "rccl"
+
+
+@pytest.mark.parametrize("extra", [[], ["--no-relabel"], ["--sort-rows"]])
+def test_python_cli_gpu(tmp_path, msbfs_pkg, extra):
+    """`python -m msbfs` (the torch.distributed twin) on the GPU: degree relabelling on by
+    default, the 7-line report and the F vector equal to the CPU oracle."""
+    import sys
+    m = msbfs_pkg
+    g, qs, gp, qp = _files(tmp_path, m, 90, 3)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    r = _run([sys.executable, "-m", "msbfs", "-g", gp, "-q", qp, "-gn", "1", "--algo", "bitpar",
+              "--json"] + extra, {"PYTHONPATH": ROOT})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.splitlines()
+    k = m.argmin_first(ref.F)
+    assert lines[2] == f"Query number (k) with minimum F value: {k + 1}"
+    assert lines[3] == f"Minimum F value: {ref.F[k]}"
+    js = json.loads(lines[7])
+    assert js["F"] == list(map(int, ref.F)) and js["traversed_edges"] == int(ref.edges.sum())
