@@ -288,6 +288,47 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
   }
 }
 
+// k_level_reduce over the slab rows of nlev consecutive levels (`rows` rows each, level j's rows
+// first-level-major) of the device-driven batches: F += sum_j weight(level_first + j) * count_j;
+// alive_next = the groups with new vertices at the last of them. One launch per few levels (a
+// launch costs ~5 us, a road-like graph's level 15-200 us); the levels in between read an older
+// alive mask, a superset, which only lets them mark fewer vertices done.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_level_reduce_multi(const uint32_t* slabF, int rows,
+                                                               int nlev, int rgroups,
+                                                               uint32_t level_first, int weight_l1,
+                                                               unsigned long long* F,
+                                                               uint64_t* alive_next) {
+  __shared__ unsigned long long pf[kWaves][64];
+  __shared__ uint32_t pl[kWaves][64];
+  const int word = blockIdx.x % W, rg = blockIdx.x / W;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  const int r0 = (int)((int64_t)rows * rg / rgroups);
+  const int r1 = (int)((int64_t)rows * (rg + 1) / rgroups);
+  const int i = word * 64 + lane;
+  unsigned long long fw = 0;
+  uint32_t last = 0;
+  for (int j = 0; j < nlev; ++j) {
+    uint32_t f = 0;
+    for (int r = r0 + wv; r < r1; r += kWaves) f += slabF[((size_t)j * rows + r) * (64 * W) + i];
+    const uint32_t lvl = level_first + (uint32_t)j;
+    fw += (unsigned long long)f * ((lvl == 1 && !weight_l1) ? 0u : lvl);
+    last = f;
+  }
+  pf[wv][lane] = fw;
+  pl[wv][lane] = last;
+  __syncthreads();
+  if (wv == 0) {
+    for (int w = 1; w < kWaves; ++w) {
+      fw += pf[w][lane];
+      last += pl[w][lane];
+    }
+    if (fw) atomicAdd(&F[i], fw);
+    const uint64_t m = __ballot(last != 0);
+    if (lane == 0 && m) atomicOr((unsigned long long*)&alive_next[word], m);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // init: scatter the batch's sources (v, local group) into both visited buffers and the
 // top-down accumulator; dedupe vertices into the first frontier list via stamps.
@@ -524,8 +565,12 @@ __global__ __launch_bounds__(kBlock) void k_td_expand_small(
 }
 
 // device-driven level batch: seed slot 0 with the current frontier size and alive mask
-__global__ void k_batch_seed(Ctr* c0, uint32_t nf, const uint64_t* alive, uint64_t* alive0) {
-  if (threadIdx.x == 0) c0->fl2.v = nf;
+__global__ void k_batch_seed(Ctr* c0, uint32_t nf, unsigned long long ef, const uint64_t* alive,
+                             uint64_t* alive0) {
+  if (threadIdx.x == 0) {
+    c0->fl2.v = nf;
+    c0->ef2.v = ef;
+  }
   if (threadIdx.x < 16) alive0[threadIdx.x] = alive[threadIdx.x];
 }
 
@@ -630,6 +675,205 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
       if (idx < nf_old) stv<VW>(accCur_zero + (int64_t)fl_old[idx] * W + slot * VW, vzero<VW>());
     }
   }
+}
+
+// One-kernel top-down level for low-degree graphs (device-driven batches, td_batch; road-like
+// graphs run thousands of levels of up to a few million frontier vertices, where the expand +
+// finalize pair spent ~115 us per level, much of it on chains of dependent loads).
+// The visited row itself is the claim: atomicOr(vis[v], frontier bits) returns the bits other
+// pushers already set, so every (vertex, group) bit is counted exactly once, by the push that
+// set it; the new bits go to accNext (the next frontier's bits) and the push that finds accNext
+// empty (W = 1) or wins the stamp (W > 1) appends v to the next frontier. No touched list and
+// no second pass; only vis[cur] is updated (the caller marks the other buffer stale, see
+// Loop::old_stale). Each lane walks U edges of its vertex per step with all loads issued
+// before the atomics. Requires fully valid rows of vis[cur] (no lazy batch) and frontier bits
+// in accCur, which the lane that reads them clears (accCur is the level-after-next's accNext).
+// The next frontier is written twice: as a list (flNext, its size is the next level's nf) and
+// as a bitmap (fbmNext). Levels with at least bm_min frontier vertices walk the bitmap instead
+// of the list: blocks expand the set bits of 256 consecutive words (8192 ids) in id order, so
+// the rows, row offsets and neighbour rows a block touches are contiguous runs (a grid graph's
+// neighbours are v +- 1 and v +- width) instead of the list's arrival order. The level consumes
+// (zeroes) fbmCur either way. Frontier degree sums: level i adds its own frontier's (from the
+// row offsets it loads anyway) to the previous slot's ef (own: that slot's frontier was written
+// by a fused level); only the batch's last level (tail) sums the degrees of what it appends.
+// Road grid 4896^2, 64 groups (MI355X): expand + finalize 562 ms; one kernel 371 ms; + bitmap
+// walk 334 ms; + both atomics in flight, deferred degree sums, one reduction per 6 levels 319 ms.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_td_fused(
+    const int32_t* fl, const uint32_t* nf_dev, int64_t bm_min, uint32_t* fbmCur,
+    uint32_t* fbmNext, int64_t nwords, const int64_t* rowptr, const int32_t* col, uint64_t* vis,
+    uint64_t* accCur, uint64_t* accNext, const uint64_t* alive, const uint64_t* gmask,
+    uint32_t* done, uint32_t* anyvis, int32_t* stamp, int32_t epoch, int32_t* flNext, Ctr* ctr,
+    uint32_t* slabF, Ctr* cprev, int own, int tail) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  constexpr int U = 4;
+  constexpr int QC = 2 * kQCap;
+  static_assert(TILE * U <= QC / 2, "queue room for one step");
+  __shared__ LdsQueueN<QC> q;
+  __shared__ unsigned long long scratch[kWaves];
+  constexpr int CR = 65;  // bank-skewed counter rows (see BitCounter::spill_strided)
+  __shared__ uint32_t cnt[CR * W];
+  // bitmap mode: words per tile (8192 ids; 4096-id tiles measured 6 % slower on the road grid)
+  constexpr int BW = kBlock;
+  __shared__ uint16_t lst[BW * 32];  // bitmap mode: set bits of the tile's words
+  __shared__ uint32_t wsum[kWaves];
+  for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
+  q_init(q);
+  __syncthreads();
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
+  const int64_t nf = (int64_t)*nf_dev;
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  V<VW> amg;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) amg.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  unsigned long long ef = 0, ev = 0, ef_own = 0;
+
+  // expand frontier vertex u (has) of this lane's row group; block-uniform call
+  auto expand = [&](bool has, int32_t u) {
+    int64_t e = 0, end = 0;
+    V<VW> fb = vzero<VW>();
+    if (has) {
+      e = rowptr[u];
+      end = rowptr[u + 1];
+      if (slot == 0) ef_own += (unsigned long long)(end - e);
+      const int64_t uo = (int64_t)u * W + slot * VW;
+      fb = ldv<VW>(accCur + uo);
+      stv<VW>(accCur + uo, vzero<VW>());
+    }
+    while (__syncthreads_or(e < end)) {
+      int32_t v[U];
+      uint32_t dw[U];
+      V<VW> r[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) v[j] = e + j < end ? col[e + j] : -1;
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        dw[j] = ~0u;
+        r[j] = vzero<VW>();
+        if (v[j] >= 0) {
+          dw[j] = done[v[j] >> 5];
+          r[j] = ldv<VW>(vis + (int64_t)v[j] * W + slot * VW);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int32_t x = v[j];
+        V<VW> nw = vzero<VW>();
+        bool push = false, first = false, full = true, was0 = true;
+        if (x >= 0 && !((dw[j] >> (x & 31)) & 1u)) {
+          const int64_t xo = (int64_t)x * W + slot * VW;
+#pragma unroll
+          for (int k = 0; k < VW; ++k) {
+            const uint64_t mm = fb.w[k] & ~r[j].w[k];
+            uint64_t now = r[j].w[k];
+            if (mm) {
+              // both atomics in flight together: accNext may take a bit a concurrent push
+              // claimed in vis first (that push adds it too: same union); the vis return
+              // decides which push counts it
+              const uint64_t ov = atomicOr((unsigned long long*)&vis[xo + k], mm);
+              const uint64_t oa = atomicOr((unsigned long long*)&accNext[xo + k], mm);
+              nw.w[k] = mm & ~ov;
+              now = ov | mm;
+              first |= oa == 0ull;
+              was0 &= ov == 0ull;
+              push = true;
+            }
+            full &= (~now & amg.w[k]) == 0;
+          }
+        }
+        // one lane per row group decides for the vertex (the G lanes share x)
+        const uint64_t bg = __ballot(push), bn = __ballot(!full);
+        const bool g_push = (bg >> (sub * G)) & L::GBITS;
+        const bool g_full = !((bn >> (sub * G)) & L::GBITS);
+        const bool leader = slot == 0 && g_push;
+        bool app = false, fresh = false;
+        if (leader) {
+          const uint32_t bit = 1u << (x & 31);
+          if constexpr (W == 1) {
+            app = first;  // accNext was empty: v's first touch this level
+            // the whole row was empty (vis is cleared per batch): first visit by any group
+            fresh = was0;
+            if (fresh) atomicOr(&anyvis[x >> 5], bit);
+          } else {
+            app = atomicExch(&stamp[x], epoch) != epoch;
+            if (!any_visited(anyvis, x)) fresh = !(atomicOr(&anyvis[x >> 5], bit) & bit);
+          }
+          if (g_full) set_done(done, x);
+          if (app) atomicOr(&fbmNext[x >> 5], bit);
+          // the next frontier's degree sum is taken by the next level from the row offsets it
+          // loads anyway (ef_own), except after the batch's last level
+          if ((app && tail) || fresh) {
+            const unsigned long long deg = (unsigned long long)(rowptr[x + 1] - rowptr[x]);
+            if (app && tail) ef += deg;
+            if (fresh) ev += deg;
+          }
+        }
+        bc.add(nw);
+        if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+          bc.template spill_strided<CR>(cnt, slot);
+          nadd = 0;
+        }
+        q_push(q, app, x);
+      }
+      q_flush(q, flNext, &ctr->fl2.v, TILE * U, false);
+      e += U;
+    }
+  };
+
+  if (nf < bm_min) {
+    for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nf; tb += (int64_t)gridDim.x * TILE) {
+      const int64_t idx = tb + wv * VPW + sub;
+      const bool has = idx < nf;
+      const int32_t u = has ? fl[idx] : 0;
+      if (has && slot == 0) fbmCur[u >> 5] = 0u;  // (every bit of the word is in this list)
+      expand(has, u);
+    }
+  } else {
+    for (int64_t wb = (int64_t)blockIdx.x * BW; wb < nwords; wb += (int64_t)gridDim.x * BW) {
+      const int64_t wi = wb + threadIdx.x;
+      const uint32_t w = (threadIdx.x < BW && wi < nwords) ? fbmCur[wi] : 0u;
+      if (!__syncthreads_or(w != 0u)) continue;
+      if (w) fbmCur[wi] = 0u;
+      // block exclusive scan of the words' popcounts -> positions in lst
+      const uint32_t c = (uint32_t)__popc(w);
+      uint32_t incl = c;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) wsum[wv] = incl;
+      __syncthreads();
+      uint32_t base = 0, total = 0;
+#pragma unroll
+      for (int k = 0; k < kWaves; ++k) {
+        base += k < wv ? wsum[k] : 0u;
+        total += wsum[k];
+      }
+      uint32_t pos = base + incl - c;
+      for (uint32_t x = w; x; x &= x - 1)
+        lst[pos++] = (uint16_t)((threadIdx.x << 5) + (__ffs(x) - 1));
+      __syncthreads();
+      for (uint32_t c0 = 0; c0 < total; c0 += TILE) {
+        const uint32_t idx = c0 + wv * VPW + sub;
+        const bool has = idx < total;
+        expand(has, has ? (int32_t)(wb * 32 + lst[idx]) : 0);
+      }
+      __syncthreads();  // lst / wsum reused by the next tile
+    }
+  }
+  q_flush(q, flNext, &ctr->fl2.v, 0, true);
+  if (tail) block_sum_add(ef, &ctr->ef2.v, scratch);
+  if (own) block_sum_add(ef_own, &cprev->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
+  bc.template spill_strided<CR>(cnt, slot);
+  __syncthreads();
+  uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+  for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
 }
 
 template <int W>
@@ -1813,6 +2057,11 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_COOP")) coop_ = atoi(x);
     if (const char* x = getenv("MSBFS_GAMMA")) gamma_ = atof(x);
     if (const char* x = getenv("MSBFS_LAZY")) lazy_ = atoi(x);
+    if (const char* x = getenv("MSBFS_TD_FUSED")) td_fused_ = atoi(x);
+    if (const char* x = getenv("MSBFS_TD_BM")) td_bm_min_ = atoll(x);
+    if (const char* x = getenv("MSBFS_TD_RED")) td_red_ = atoi(x);
+    if (const char* x = getenv("MSBFS_TD_GRID"))
+      td_grid_ = std::max(1, std::min(3 * kMaxGrid, atoi(x)));  // (slab rows)
     if (const char* x = getenv("MSBFS_AQ")) aq_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX_H")) pfx_h_ = atoi(x);
     if (const char* x = getenv("MSBFS_CODE_DEG")) code_deg_ = atof(x);
@@ -1918,6 +2167,7 @@ class BitparSolver final : public Solver {
     bool osnap_next = false;            // the previous level was the first pull of a lazy batch
     bool lean_off = false;              // a lean first-row pass overflowed (see k_bu_first)
     bool lean_ran = false;              // this level ran one (its overflow count is c.touched)
+    bool old_stale = false;             // k_td_fused levels updated only vis_[cur]
   };
   struct Small {
     unsigned long long* F;
@@ -1942,6 +2192,12 @@ class BitparSolver final : public Solver {
   void levels(Loop& S, RunStats* st, hipStream_t s);
   template <int W, bool COUNT>
   void td_batch(Loop& S, RunStats* st, hipStream_t s);
+  // device-driven top-down batches run k_td_fused levels (needs every row of vis_[cur] valid,
+  // i.e. no lazy batch; the edge-counting pass keeps expand + finalize + k_count_frontier)
+  template <bool COUNT>
+  bool fused_batches() const {
+    return !COUNT && td_fused_ && batch_levels_ > 1 && g_.max_degree <= kSmallDeg;
+  }
   template <int W, bool COUNT>
   void batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids, int64_t* F,
                   int64_t* edges2, RunStats* st, hipStream_t s);
@@ -2050,6 +2306,11 @@ class BitparSolver final : public Solver {
   int32_t pfx_h_ = 0;  // MSBFS_PFX_H: lower prefix bound (tuning; smaller measured slower)
   int aq_ = 4096;       // MSBFS_AQ: vertices per block of the active-list build (4096 or 1024)
   int lazy_ = 1;        // MSBFS_LAZY=0: every batch fills vis_[0] (see start_batch)
+  int td_fused_ = 1;    // MSBFS_TD_FUSED=0: device-driven batches use expand + finalize
+  int64_t td_bm_min_ = 65536;  // MSBFS_TD_BM: k_td_fused walks the frontier bitmap from this nf
+  DevBuf fbm_[2];       // frontier bitmaps of the fused levels (n bits each)
+  int td_grid_ = 1024;  // MSBFS_TD_GRID: blocks of the device-driven batches' kernels
+  int td_red_ = 6;      // MSBFS_TD_RED: fused levels per k_level_reduce_multi launch
   DevBuf asnap_;        // any-visited bitmap at the start of a lazy batch's first pull level
   double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
   int coop_ = -1;      // MSBFS_COOP: cross-chunk early exit on the first pull level (-1 auto)
@@ -2270,6 +2531,13 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       if (st) st->td_levels++;
     } else {
       // ---- bottom-up
+      if (S.old_stale) {
+        // fused top-down levels wrote only vis_[cur]; pulls write the other buffer's rows of the
+        // active vertices and read both buffers' rows of the finished ones afterwards
+        const size_t vb = (size_t)std::max<int64_t>(n_eff(), 1) * W * sizeof(uint64_t);
+        MSBFS_HIP_CHECK(hipMemcpyAsync(O, R, vb, hipMemcpyDeviceToDevice, s));
+        S.old_stale = false;
+      }
       const int next_wide = std::max(opt.wide_degree, wide_later_);
       if (!S.have_active) {
         // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
@@ -2569,21 +2837,67 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
   Ctr* slots = bctr_.as<Ctr>();
   uint64_t* aslot = (uint64_t*)(slots + kBatch + 1);
   MSBFS_HIP_CHECK(hipMemsetAsync(bctr_.p, 0, bctr_.bytes, s));
-  k_batch_seed<<<1, 64, 0, s>>>(slots, (uint32_t)S.nf, sm.alive[S.alv], aslot);
+  const int64_t nwords = (n_eff() + 31) / 32;
+  if (fused_batches<COUNT>()) {
+    // the batch's first level reads the host's list; later ones may walk the bitmap its
+    // predecessor wrote (levels outside the batch leave stale bits: start from zero)
+    for (auto& b : fbm_) {
+      b.ensure((size_t)std::max<int64_t>(nwords, 1) * sizeof(uint32_t));
+      MSBFS_HIP_CHECK(hipMemsetAsync(b.p, 0, (size_t)std::max<int64_t>(nwords, 1) * 4, s));
+    }
+  }
+  k_batch_seed<<<1, 64, 0, s>>>(slots, (uint32_t)S.nf, (unsigned long long)S.ef,
+                                sm.alive[S.alv], aslot);
   MSBFS_HIP_CHECK(hipGetLastError());
   constexpr bool FUSE = !COUNT;
   const bool fuse = FUSE && fuse_count_;
-  const int grid = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + L::TILE - 1) / L::TILE));
+  const int grid = (int)std::min<int64_t>(td_grid_, std::max<int64_t>(1, (n + L::TILE - 1) / L::TILE));
   uint64_t* R = vis_[S.cur].as<uint64_t>();
   uint64_t* O = vis_[S.cur ^ 1].as<uint64_t>();
   const uint32_t level0 = S.level;
   const auto t0 = std::chrono::steady_clock::now();
+  bool bm_ok = false;  // the previous level of this batch wrote the frontier bitmap
+  const int rg = std::max(1, std::min(64, grid / 32));
+  // fused levels share a reduction launch: level i's counters go to slab rows (i - pend) * grid
+  const int red = std::max(1, std::min(td_red_, 3 * kMaxGrid / grid));
+  int pend = -1;  // first fused level not reduced yet
+  int aidx = 0;   // alive slot the next level reads
+  auto reduce_pending = [&](int upto) {
+    if (pend < 0) return;
+    k_level_reduce_multi<W><<<W * rg, kBlock, 0, s>>>(slabF_.as<uint32_t>(), grid, upto - pend,
+                                                      rg, level0 + 1 + pend, S.weight_l1 ? 1 : 0,
+                                                      sm.F, aslot + 16 * upto);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    aidx = upto;
+    pend = -1;
+  };
   trace::Range range_batch("bitpar L%u-%u TD batch", level0 + 1, level0 + K);
   for (int i = 0; i < K; ++i) {
     Ctr* prev = slots + i;
     Ctr* cur = slots + i + 1;
     const uint32_t level = level0 + 1 + i;
     ++epoch_;
+    const uint32_t weight = (level == 1 && !S.weight_l1) ? 0u : level;
+    if (fused_batches<COUNT>() && S.fsrc_acc && !S.lazy) {
+      if (pend < 0) pend = i;
+      k_td_fused<W><<<grid, kBlock, 0, s>>>(
+          fl_[S.fc].as<int32_t>(), &prev->fl2.v, bm_ok ? td_bm_min_ : INT64_MAX,
+          fbm_[S.fc & 1].as<uint32_t>(), fbm_[(S.fc & 1) ^ 1].as<uint32_t>(), nwords, g_.rowptr,
+          g_.col, R, acc_[S.ac].as<uint64_t>(), acc_[S.ac ^ 1].as<uint64_t>(), aslot + 16 * aidx,
+          sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), stamp_.as<int32_t>(), epoch_,
+          fl_[S.fc ^ 1].as<int32_t>(), cur,
+          slabF_.as<uint32_t>() + (size_t)(i - pend) * grid * 64 * W, prev,
+          bm_ok ? 1 : 0, i + 1 == K ? 1 : 0);
+      MSBFS_HIP_CHECK(hipGetLastError());
+      if (i + 1 - pend == red || i + 1 == K) reduce_pending(i + 1);
+      S.fc ^= 1;
+      S.ac ^= 1;
+      S.old_stale = true;
+      bm_ok = true;
+      continue;
+    }
+    reduce_pending(i);
+    bm_ok = false;  // (this level writes no bitmap)
     if (S.fsrc_acc)
       k_td_expand_small<W, false><<<grid, kBlock, 0, s>>>(
           fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v, g_.rowptr, g_.col, R,
@@ -2598,7 +2912,7 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
           S.osnap_next ? asnap_.as<uint32_t>() : nullptr);
     auto kf = fuse ? k_td_finalize<W, COUNT, FUSE> : k_td_finalize<W, COUNT, false>;
     kf<<<grid, kBlock, 0, s>>>(touched_.as<int32_t>(), g_.rowptr, R, O,
-                               acc_[S.ac ^ 1].as<uint64_t>(), aslot + 16 * i, sm.gmask,
+                               acc_[S.ac ^ 1].as<uint64_t>(), aslot + 16 * aidx, sm.gmask,
                                done_.as<uint32_t>(), fl_[S.fc ^ 1].as<int32_t>(), cur,
                                fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v,
                                S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr,
@@ -2607,19 +2921,18 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
       k_count_frontier<W, COUNT, false><<<grid, kBlock, 0, s>>>(
           fl_[S.fc ^ 1].as<int32_t>(), cur, g_.rowptr, acc_[S.ac ^ 1].as<uint64_t>(), nullptr,
           slabF_.as<uint32_t>(), slabE_.as<unsigned long long>());
-    const int rg = std::max(1, std::min(64, grid / 32));
-    const uint32_t weight = (level == 1 && !S.weight_l1) ? 0u : level;
     k_level_reduce<W, COUNT><<<W * rg, kBlock, 0, s>>>(slabF_.as<uint32_t>(),
                                                        slabE_.as<unsigned long long>(), grid, rg,
                                                        sm.F, sm.E, aslot + 16 * (i + 1), weight);
     MSBFS_HIP_CHECK(hipGetLastError());
+    aidx = i + 1;
     S.fc ^= 1;
     S.ac ^= 1;
     S.fsrc_acc = true;
     S.osnap_next = false;
   }
   // alive after the batch -> the host loop's current alive buffer
-  MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[S.alv], aslot + 16 * K, 16 * sizeof(uint64_t),
+  MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[S.alv], aslot + 16 * aidx, 16 * sizeof(uint64_t),
                                  hipMemcpyDeviceToDevice, s));
   MSBFS_HIP_CHECK(hipMemcpyAsync(hbctr_->p, bctr_.p, (size_t)(K + 1) * sizeof(Ctr),
                                  hipMemcpyDeviceToHost, s));
@@ -2669,7 +2982,7 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
   S.cnt = n_eff();
   // lazy: no per-batch fill of vis_[0] (n_eff * 8W bytes, ~0.8 ms on RMAT-26); the edge-counting
   // pass re-reads both rows of every new vertex (k_count_frontier), so it keeps the fill
-  S.lazy = lazy_ && !COUNT && fuse_count_;
+  S.lazy = lazy_ && !COUNT && fuse_count_ && !fused_batches<COUNT>();
   start_batch<W, COUNT>(k0, nb, qoff, qids, S, s);
   levels<W, COUNT>(S, st, s);
   // frontier is empty: accumulator entries were cleared by finalize / zero_acc

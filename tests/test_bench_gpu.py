@@ -36,3 +36,40 @@ def test_bench_forced_rccl_one_rank(dist):
         assert js["config"]["parallelism"].startswith("hybrid1")
     if dist == "auto":
         assert set(js["config"]["candidates_ms"]) == {"roundrobin", "hybrid"}
+
+
+def test_bench_graph_forced_rccl_one_rank(msbfs_pkg):
+    """tools/bench_graph.py (secondary BASELINE configs) through a one-rank RCCL group: round
+    robin split, the packed all-reduce(MIN), the answer equal to the CPU oracle's."""
+    msbfs = msbfs_pkg
+    env = dict(os.environ, MSBFS_FORCE_DIST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
+               RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_graph.py"), "--graph",
+                        "grid:200:200:0.7", "--groups", "100", "--group-size", "4", "--steps", "2",
+                        "--verify", "4"], capture_output=True, text=True, env=env, timeout=110,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    g = msbfs.Graph.grid(200, 200, 0.7, 0, 1)
+    ref = msbfs.cpu_bfs(g, msbfs.QuerySet.random(g.n, 100, 4, 7), count_edges=True)
+    k = msbfs.argmin_first(ref.F)
+    assert js["n_gpus"] == 1 and js["min_k"] == k + 1 and js["min_f"] == int(ref.F[k])
+    assert js["traversed_edges"] == int(ref.edges.sum())
+
+
+def test_bench_graph_two_ranks_gloo(msbfs_pkg):
+    """Two ranks sharing the GPU (gloo host collectives): each rank runs half of the groups."""
+    msbfs = msbfs_pkg
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(_port()), os.path.join(ROOT, "tools", "bench_graph.py"), "--graph",
+                        "rmat:14:8", "--relabel", "1", "--groups", "130", "--group-size", "3",
+                        "--steps", "1", "--backend", "gloo"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    g = msbfs.Graph.rmat(14, 8, 1)
+    ref = msbfs.cpu_bfs(g, msbfs.QuerySet.random(g.n, 130, 3, 7), count_edges=True)
+    k = msbfs.argmin_first(ref.F)
+    assert js["n_gpus"] == 2 and js["min_k"] == k + 1 and js["min_f"] == int(ref.F[k])
+    assert js["traversed_edges"] == int(ref.edges.sum())
