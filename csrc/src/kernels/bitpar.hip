@@ -290,16 +290,15 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
 
 // k_level_reduce over the slab rows of nlev consecutive levels (`rows` rows each, level j's rows
 // first-level-major) of the device-driven batches: F += sum_j weight(level_first + j) * count_j;
-// alive_next = the groups with new vertices at the last of them. One launch per few levels (a
-// launch costs ~5 us, a road-like graph's level 15-200 us); the levels in between read an older
-// alive mask, a superset, which only lets them mark fewer vertices done.
+// alive_next + 16 * j = the groups with new vertices at level j (the mask after it). One launch
+// per few levels (a launch costs ~5 us, a road-like graph's level 15-200 us); the levels in
+// between read an older alive mask, a superset, which only lets them mark fewer vertices done.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_level_reduce_multi(const uint32_t* slabF, int rows,
                                                                int nlev, int rgroups,
                                                                uint32_t level_first, int weight_l1,
                                                                unsigned long long* F,
                                                                uint64_t* alive_next) {
-  __shared__ unsigned long long pf[kWaves][64];
   __shared__ uint32_t pl[kWaves][64];
   const int word = blockIdx.x % W, rg = blockIdx.x / W;
   const int lane = lane_id(), wv = threadIdx.x >> 6;
@@ -307,26 +306,21 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce_multi(const uint32_t* s
   const int r1 = (int)((int64_t)rows * (rg + 1) / rgroups);
   const int i = word * 64 + lane;
   unsigned long long fw = 0;
-  uint32_t last = 0;
   for (int j = 0; j < nlev; ++j) {
     uint32_t f = 0;
     for (int r = r0 + wv; r < r1; r += kWaves) f += slabF[((size_t)j * rows + r) * (64 * W) + i];
-    const uint32_t lvl = level_first + (uint32_t)j;
-    fw += (unsigned long long)f * ((lvl == 1 && !weight_l1) ? 0u : lvl);
-    last = f;
-  }
-  pf[wv][lane] = fw;
-  pl[wv][lane] = last;
-  __syncthreads();
-  if (wv == 0) {
-    for (int w = 1; w < kWaves; ++w) {
-      fw += pf[w][lane];
-      last += pl[w][lane];
+    pl[wv][lane] = f;
+    __syncthreads();
+    if (wv == 0) {
+      for (int w = 1; w < kWaves; ++w) f += pl[w][lane];
+      const uint32_t lvl = level_first + (uint32_t)j;
+      fw += (unsigned long long)f * ((lvl == 1 && !weight_l1) ? 0u : lvl);
+      const uint64_t m = __ballot(f != 0);
+      if (lane == 0 && m) atomicOr((unsigned long long*)&alive_next[16 * j + word], m);
     }
-    if (fw) atomicAdd(&F[i], fw);
-    const uint64_t m = __ballot(last != 0);
-    if (lane == 0 && m) atomicOr((unsigned long long*)&alive_next[word], m);
+    __syncthreads();
   }
+  if (wv == 0 && fw) atomicAdd(&F[i], fw);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -499,9 +493,16 @@ __global__ __launch_bounds__(kBlock) void k_td_expand_small(
     const int32_t* fl, int64_t nf_arg, const uint32_t* nf_dev, const int64_t* rowptr,
     const int32_t* col, const uint64_t* visCur, const uint64_t* fsrc, const uint32_t* done,
     uint64_t* accNext, int32_t* stamp, int32_t epoch, int32_t* touched, Ctr* ctr,
-    const uint32_t* lzv = nullptr, const uint32_t* osnap = nullptr) {
+    const uint32_t* lzv = nullptr, const uint32_t* osnap = nullptr, Ctr* cstop = nullptr,
+    unsigned long long ef_stop = 0) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  // device-driven batch: stop where the host would pull (cstop = the slot of this level's
+  // frontier, whose degree sum the previous finalize wrote; see k_td_fused)
+  if (cstop && cstop->fl2.v > 0 && cstop->ef2.v > ef_stop) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) cstop->act2.v = 1u;
+    return;
+  }
   __shared__ LdsQueue q;
   q_init(q);
   __syncthreads();
@@ -582,8 +583,13 @@ __global__ __launch_bounds__(kBlock) void k_td_finalize(
     const int32_t* touched, const int64_t* rowptr, uint64_t* visCur, uint64_t* visOld,
     uint64_t* accNext, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* fl2,
     Ctr* ctr, const int32_t* fl_old, int64_t nf_old_arg, const uint32_t* nfold_dev,
-    uint64_t* accCur_zero, uint32_t* anyvis, uint32_t* slabF, int lazy) {
+    uint64_t* accCur_zero, uint32_t* anyvis, uint32_t* slabF, int lazy, const uint32_t* stop) {
   static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
+  if (stop && *stop) {  // the batch stopped at this level (k_td_expand_small)
+    if constexpr (FUSE)
+      for (int i = threadIdx.x; i < 64 * W; i += kBlock) slabF[(size_t)blockIdx.x * 64 * W + i] = 0u;
+    return;
+  }
   const int64_t nf_old = nfold_dev ? (int64_t)*nfold_dev : nf_old_arg;
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
@@ -704,7 +710,8 @@ __global__ __launch_bounds__(kBlock) void k_td_fused(
     uint32_t* fbmNext, int64_t nwords, const int64_t* rowptr, const int32_t* col, uint64_t* vis,
     uint64_t* accCur, uint64_t* accNext, const uint64_t* alive, const uint64_t* gmask,
     uint32_t* done, uint32_t* anyvis, int32_t* stamp, int32_t epoch, int32_t* flNext, Ctr* ctr,
-    uint32_t* slabF, Ctr* cprev, int own, int tail) {
+    uint32_t* slabF, Ctr* cprev, int own, int tail, const Ctr* cpp,
+    unsigned long long ef_stop) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   constexpr int U = 4;
@@ -731,6 +738,26 @@ __global__ __launch_bounds__(kBlock) void k_td_fused(
 #pragma unroll
   for (int j = 0; j < VW; ++j) amg.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long ef = 0, ev = 0, ef_own = 0;
+  // direction check inside the batch (the host's test, on this frontier's degree sum estimated
+  // from its size and the previous frontier's mean degree): a level the host would run as a pull
+  // does nothing but record its frontier's degree sum and the stop; every later
+  // level of the batch then sees an empty frontier, and the host resumes from this level
+  // (cprev->act2 = 1)
+  if (cpp && nf > 0 && cpp->fl2.v > 0 &&
+      (double)nf * ((double)cpp->ef2.v / (double)cpp->fl2.v) > (double)ef_stop) {
+    if (own) {
+      for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nf;
+           i += (int64_t)gridDim.x * kBlock) {
+        const int32_t u = fl[i];
+        ef_own += (unsigned long long)(rowptr[u + 1] - rowptr[u]);
+      }
+      block_sum_add(ef_own, &cprev->ef2.v, scratch);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) cprev->act2.v = 1u;  // (unused by top-down levels)
+    uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = 0u;
+    return;
+  }
 
   // expand frontier vertex u (has) of this lane's row group; block-uniform call
   auto expand = [&](bool has, int32_t u) {
@@ -2060,6 +2087,8 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_TD_FUSED")) td_fused_ = atoi(x);
     if (const char* x = getenv("MSBFS_TD_BM")) td_bm_min_ = atoll(x);
     if (const char* x = getenv("MSBFS_TD_RED")) td_red_ = atoi(x);
+    if (const char* x = getenv("MSBFS_ALPHA_LOW")) alpha_low_ = atof(x);
+    if (const char* x = getenv("MSBFS_TD_FUSED_DEG")) td_fused_deg_ = atof(x);
     if (const char* x = getenv("MSBFS_TD_GRID"))
       td_grid_ = std::max(1, std::min(3 * kMaxGrid, atoi(x)));  // (slab rows)
     if (const char* x = getenv("MSBFS_AQ")) aq_ = atoi(x);
@@ -2194,9 +2223,13 @@ class BitparSolver final : public Solver {
   void td_batch(Loop& S, RunStats* st, hipStream_t s);
   // device-driven top-down batches run k_td_fused levels (needs every row of vis_[cur] valid,
   // i.e. no lazy batch; the edge-counting pass keeps expand + finalize + k_count_frontier)
+  double alpha_eff() const {
+    return fused_batches<false>() ? std::min(opt.alpha, alpha_low_) : opt.alpha;
+  }
   template <bool COUNT>
   bool fused_batches() const {
-    return !COUNT && td_fused_ && batch_levels_ > 1 && g_.max_degree <= kSmallDeg;
+    return !COUNT && td_fused_ && batch_levels_ > 1 && g_.max_degree <= kSmallDeg &&
+           (double)g_.nnz <= td_fused_deg_ * (double)std::max<int64_t>(g_.n, 1);
   }
   template <int W, bool COUNT>
   void batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids, int64_t* F,
@@ -2311,6 +2344,15 @@ class BitparSolver final : public Solver {
   DevBuf fbm_[2];       // frontier bitmaps of the fused levels (n bits each)
   int td_grid_ = 1024;  // MSBFS_TD_GRID: blocks of the device-driven batches' kernels
   int td_red_ = 6;      // MSBFS_TD_RED: fused levels per k_level_reduce_multi launch
+  // MSBFS_TD_FUSED_DEG: fused levels only below this mean degree (road-like graphs). Denser
+  // low-degree graphs pull after a few levels, and their first pull runs faster after lazy push
+  // levels (uniform n = 16M, m = 128M, 1024 groups: 29.6 ms vs 32.3 ms with fused levels)
+  double td_fused_deg_ = 8.0;
+  // MSBFS_ALPHA_LOW: push -> pull threshold (Beamer's alpha) on graphs with max degree <= kSmallDeg
+  // (fused top-down levels). Road grid 4896^2, 256 groups: alpha 14 pulls from ~1.7M frontier
+  // vertices on and takes 3030 ms, alpha 4 stays top-down (1648 ms batched); 1024 groups still pull
+  // (8.8 s vs 12.5 s top-down only); uniform n = 16M, m = 128M, 1024 groups: pulls from level 2
+  double alpha_low_ = 4.0;
   DevBuf asnap_;        // any-visited bitmap at the start of a lazy batch's first pull level
   double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
   int coop_ = -1;      // MSBFS_COOP: cross-chunk early exit on the first pull level (-1 auto)
@@ -2438,9 +2480,9 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       // frontier edge, so pull once the frontier has more edges than the graph has vertices
       // (RMAT-30, 256 groups: 742 -> 294 ms/step; RMAT-26, 16 groups: 16.4 -> 9.3 ms; road
       // graphs never get there). MSBFS_GAMMA scales the vertex test (0 turns it off).
-      bottom_up = (double)S.ef > (double)S.ea / opt.alpha ||
+      bottom_up = (double)S.ef > (double)S.ea / alpha_eff() ||
                   (gamma_ > 0 && S.level >= 1 && (double)S.ef > gamma_ * (double)n_eff());
-    else bottom_up = !((double)S.nf < (double)S.na / opt.beta && (double)S.ef < (double)S.ea / opt.alpha);
+    else bottom_up = !((double)S.nf < (double)S.na / opt.beta && (double)S.ef < (double)S.ea / alpha_eff());
     if (S.level < dirs_.size() && (dirs_[S.level] == 'T' || dirs_[S.level] == 'B'))
       bottom_up = dirs_[S.level] == 'B';
     if (S.level < S.plan.size() && (S.plan[S.level] == 'T' || S.plan[S.level] == 'B'))
@@ -2512,7 +2554,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           sm.gmask, done_.as<uint32_t>(), fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
           fl_[S.fc].as<int32_t>(), S.nf, nullptr,
           S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr, anyvis_.as<uint32_t>(), slabF(rows),
-          S.lazy ? 1 : 0);
+          S.lazy ? 1 : 0, nullptr);
       MSBFS_HIP_CHECK(hipGetLastError());
       if (fuse) {
         rows += gf;
@@ -2861,12 +2903,17 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
   // fused levels share a reduction launch: level i's counters go to slab rows (i - pend) * grid
   const int red = std::max(1, std::min(td_red_, 3 * kMaxGrid / grid));
   int pend = -1;  // first fused level not reduced yet
+  // the host's push -> pull test, on the degree sum of the frontier entering a level
+  double efs = (double)S.ea / alpha_eff();
+  if (gamma_ > 0) efs = std::min(efs, gamma_ * (double)n_eff());
+  const unsigned long long ef_stop =
+      opt.force_dir == 1 ? ~0ull : (unsigned long long)std::max(0.0, std::min(efs, 1.8e19));
   int aidx = 0;   // alive slot the next level reads
   auto reduce_pending = [&](int upto) {
     if (pend < 0) return;
     k_level_reduce_multi<W><<<W * rg, kBlock, 0, s>>>(slabF_.as<uint32_t>(), grid, upto - pend,
                                                       rg, level0 + 1 + pend, S.weight_l1 ? 1 : 0,
-                                                      sm.F, aslot + 16 * upto);
+                                                      sm.F, aslot + 16 * (pend + 1));
     MSBFS_HIP_CHECK(hipGetLastError());
     aidx = upto;
     pend = -1;
@@ -2887,7 +2934,7 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
           sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), stamp_.as<int32_t>(), epoch_,
           fl_[S.fc ^ 1].as<int32_t>(), cur,
           slabF_.as<uint32_t>() + (size_t)(i - pend) * grid * 64 * W, prev,
-          bm_ok ? 1 : 0, i + 1 == K ? 1 : 0);
+          bm_ok ? 1 : 0, i + 1 == K ? 1 : 0, i > 0 ? slots + i - 1 : nullptr, ef_stop);
       MSBFS_HIP_CHECK(hipGetLastError());
       if (i + 1 - pend == red || i + 1 == K) reduce_pending(i + 1);
       S.fc ^= 1;
@@ -2903,20 +2950,21 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
           fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v, g_.rowptr, g_.col, R,
           acc_[S.ac].as<uint64_t>(), done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(),
           stamp_.as<int32_t>(), epoch_, touched_.as<int32_t>(), cur,
-          S.lazy ? anyvis_.as<uint32_t>() : nullptr);
+          S.lazy ? anyvis_.as<uint32_t>() : nullptr, nullptr, i > 0 ? prev : nullptr, ef_stop);
     else
       k_td_expand_small<W, true><<<grid, kBlock, 0, s>>>(
           fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v, g_.rowptr, g_.col, R, O,
           done_.as<uint32_t>(), acc_[S.ac ^ 1].as<uint64_t>(), stamp_.as<int32_t>(), epoch_,
           touched_.as<int32_t>(), cur, S.lazy ? anyvis_.as<uint32_t>() : nullptr,
-          S.osnap_next ? asnap_.as<uint32_t>() : nullptr);
+          S.osnap_next ? asnap_.as<uint32_t>() : nullptr, i > 0 ? prev : nullptr, ef_stop);
     auto kf = fuse ? k_td_finalize<W, COUNT, FUSE> : k_td_finalize<W, COUNT, false>;
     kf<<<grid, kBlock, 0, s>>>(touched_.as<int32_t>(), g_.rowptr, R, O,
                                acc_[S.ac ^ 1].as<uint64_t>(), aslot + 16 * aidx, sm.gmask,
                                done_.as<uint32_t>(), fl_[S.fc ^ 1].as<int32_t>(), cur,
                                fl_[S.fc].as<int32_t>(), 0, &prev->fl2.v,
                                S.fsrc_acc ? acc_[S.ac].as<uint64_t>() : nullptr,
-                               anyvis_.as<uint32_t>(), slabF_.as<uint32_t>(), S.lazy ? 1 : 0);
+                               anyvis_.as<uint32_t>(), slabF_.as<uint32_t>(), S.lazy ? 1 : 0,
+                               &prev->act2.v);
     if (!fuse)
       k_count_frontier<W, COUNT, false><<<grid, kBlock, 0, s>>>(
           fl_[S.fc ^ 1].as<int32_t>(), cur, g_.rowptr, acc_[S.ac ^ 1].as<uint64_t>(), nullptr,
@@ -2931,26 +2979,29 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
     S.fsrc_acc = true;
     S.osnap_next = false;
   }
-  // alive after the batch -> the host loop's current alive buffer
-  MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[S.alv], aslot + 16 * aidx, 16 * sizeof(uint64_t),
-                                 hipMemcpyDeviceToDevice, s));
+  (void)aidx;
   MSBFS_HIP_CHECK(hipMemcpyAsync(hbctr_->p, bctr_.p, (size_t)(K + 1) * sizeof(Ctr),
                                  hipMemcpyDeviceToHost, s));
   MSBFS_HIP_CHECK(hipStreamSynchronize(s));
   const Ctr* h = hbctr_->as<Ctr>();
   int real = 0;
   for (int i = 0; i < K; ++i) {
-    if (h[i].fl2.v == 0) break;  // frontier empty before level i: the rest were no-ops
+    // frontier empty before level i, or level i stopped for a pull: the rest were no-ops
+    if (h[i].fl2.v == 0 || h[i].act2.v) break;
     ++real;
     S.ev += (int64_t)h[i + 1].ev2.v;
     if (level0 + 1 + i == 1) S.ev_l1 = S.ev;
   }
+  // alive after the last real level -> the host loop's current alive buffer
+  MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[S.alv], aslot + 16 * real, 16 * sizeof(uint64_t),
+                                 hipMemcpyDeviceToDevice, s));
   S.level = level0 + real;
   S.nf = h[real].fl2.v;
   S.ef = (int64_t)h[real].ef2.v;
-  if (real < K && (K - real) % 2) {
-    // the no-op levels flipped the list / accumulator parity; only matters if the loop went on,
-    // which it does not (the frontier is empty)
+  if ((K - real) % 2) {
+    // the no-op levels flipped the list / accumulator parity (they touched no buffer)
+    S.fc ^= 1;
+    S.ac ^= 1;
   }
   if (st && real > 0) {  // per-level records; the batch's wall time is split evenly
     const double ms = std::chrono::duration<double, std::milli>(

@@ -353,8 +353,9 @@ def test_device_algos_property(msbfs_pkg):
 def test_bitpar_fused_topdown_batches(msbfs_pkg, monkeypatch, fused):
     """Low-degree graphs run device-driven top-down batches; by default each level is one
     k_td_fused kernel (claims bits with atomicOr on the visited row, keeps only vis[cur] current).
-    Road-like grids stay top-down; the uniform graph switches to pulls after fused levels (the
-    stale second buffer is restored first); repeated runs reuse the buffers; W = 1, 4, 16.
+    Road-like grids stay top-down; the uniform graphs switch to pulls after fused levels (a level
+    stops the device-driven batch on the host's test; the stale second buffer is restored
+    first); repeated runs reuse the buffers; W = 1, 4, 16.
     "bitmap": the list/bitmap choice forced to the bitmap walk, short batches."""
     m = msbfs_pkg
     monkeypatch.setenv("MSBFS_TD_FUSED", "0" if fused == "0" else "1")
@@ -362,7 +363,8 @@ def test_bitpar_fused_topdown_batches(msbfs_pkg, monkeypatch, fused):
         monkeypatch.setenv("MSBFS_TD_BM", "1")
         monkeypatch.setenv("MSBFS_BATCH", "5")
     graphs = [m.Graph.grid(90, 110, 0.65, 0, 3), m.Graph.grid(50, 50, 0.9, 20, 4),
-              m.Graph.uniform(20000, 160000, 5), m.Graph.uniform(6000, 3500, 6)]
+              m.Graph.uniform(20000, 160000, 5), m.Graph.uniform(6000, 3500, 6),
+              m.Graph.uniform(60000, 240000, 7)]
     for gi, g in enumerate(graphs):
         dg = g.to_device(0)
         for K in (1, 64, 200, 1024):
@@ -377,7 +379,8 @@ def test_bitpar_fused_topdown_batches(msbfs_pkg, monkeypatch, fused):
 def test_bitpar_fused_level_records_match(msbfs_pkg, monkeypatch):
     """The fused levels take the frontier's degree sum from the next level's row offsets (and
     at a batch's last level from the appends): per-level frontier sizes and degree sums — the
-    direction heuristic's inputs — equal the expand + finalize path's."""
+    direction heuristic's inputs — equal the expand + finalize path's (push levels only: the
+    fused batches also stop for a pull on their own estimate)."""
     m = msbfs_pkg
     g = m.Graph.grid(120, 130, 0.7, 0, 5)
     dg = g.to_device(0)
@@ -387,7 +390,7 @@ def test_bitpar_fused_level_records_match(msbfs_pkg, monkeypatch):
         for fused in ("1", "0"):
             monkeypatch.setenv("MSBFS_TD_FUSED", fused)
             monkeypatch.setenv("MSBFS_BATCH", "7")
-            with m.Solver(dg, "bitpar", max_groups=K) as s:
+            with m.Solver(dg, "bitpar", max_groups=K, force_dir=1) as s:
                 s.run(qs)
                 recs[fused] = [(r["level"], r["dir"], r["nf"], r["ef"], r["nf_next"])
                                for r in s.level_trace()]
