@@ -73,3 +73,23 @@ def test_bench_graph_two_ranks_gloo(msbfs_pkg):
     k = msbfs.argmin_first(ref.F)
     assert js["n_gpus"] == 2 and js["min_k"] == k + 1 and js["min_f"] == int(ref.F[k])
     assert js["traversed_edges"] == int(ref.edges.sum())
+
+
+@pytest.mark.parametrize("ranks,dist", [(2, "hybrid"), (3, "auto")])
+def test_bench_multi_rank_gloo_shared_gpu(ranks, dist):
+    """bench.py with several ranks on the one GPU (gloo collectives, the hybrid exchange staged
+    through host memory): every rank runs its own solver, the hybrid phases exchange real
+    buffers, and bench.py checks each decomposition's F against the round-robin pass."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", str(ranks), "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--scale",
+                        "16", "--groups", "200", "--steps", "2", "--warmup", "1", "--dist", dist,
+                        "--backend", "gloo", "--verify", "4"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert js["n_gpus"] == ranks and js["value"] > 0
+    if dist == "hybrid":
+        assert js["config"]["parallelism"].startswith(f"hybrid{ranks}")
+    else:
+        assert set(js["config"]["candidates_ms"]) == {"roundrobin", "hybrid"}
