@@ -267,7 +267,8 @@ int main(int argc, char* argv[]) {
       fail("unknown --dist " + a.dist);
     const int P = comm->size(), me = comm->rank();
     int dalgo = algo;
-    if (!cpu && dalgo == 0) dalgo = (K + P - 1) / P > 1 || (a.dist == "hybrid" && K > 1) ? 1 : 2;
+    if (!cpu && dalgo == 0)
+      dalgo = a.dist == "hybrid" && K > 1 ? 1 : auto_device_algo(dg, (K + P - 1) / P);
     const bool want_hybrid =
         !cpu && dalgo == 1 && (a.dist == "hybrid" || (a.dist == "auto" && P > 1));
 

@@ -19,7 +19,7 @@ typedef struct msbfs_graph_s* msbfs_graph;
 typedef struct msbfs_solver_s* msbfs_solver;
 
 enum msbfs_algo {
-  MSBFS_ALGO_AUTO = 0,    /* bit-parallel when K > 1, else dist */
+  MSBFS_ALGO_AUTO = 0,    /* dist for <= 3 groups on graphs with max degree > 64, else bit-parallel */
   MSBFS_ALGO_BITPAR = 1,  /* 64*W groups per pass, direction optimising */
   MSBFS_ALGO_DIST = 2,    /* one distance array per group, direction optimising */
   MSBFS_ALGO_TOPDOWN = 3, /* dist path, top-down only (queue + load-balanced edges) */

@@ -342,7 +342,8 @@ int msbfs_solver_create(msbfs_graph g, int algo, int64_t max_groups, msbfs_solve
     MSBFS_HIP_CHECK(hipSetDevice(g->g.device));
     auto s = std::make_unique<msbfs_solver_s>();
     s->graph = g;
-    if (algo == MSBFS_ALGO_AUTO) algo = max_groups > 1 ? MSBFS_ALGO_BITPAR : MSBFS_ALGO_DIST;
+    if (algo == MSBFS_ALGO_AUTO)
+      algo = msbfs::auto_device_algo(g->g, max_groups) == 2 ? MSBFS_ALGO_DIST : MSBFS_ALGO_BITPAR;
     s->algo = algo;
     switch (algo) {
       case MSBFS_ALGO_BITPAR:
