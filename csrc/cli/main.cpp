@@ -389,20 +389,26 @@ int main(int argc, char* argv[]) {
                     &rs, stream);
       }
       maybe_inject("compute", comm->rank());
-      // packed (F << qbits | q) min-reduce keeps the lowest-index tie-break (main.cu:391-396)
+      // ONE packed min-reduce of 1 + (F << qbits | q) keeps the lowest-index tie-break
+      // (main.cu:391-396); a rank whose F would not fit next to the query index sends 0, so
+      // every rank sees 0 and takes the two-pass fallback together
       int qbits = 1;
       while ((int64_t(1) << qbits) <= K) ++qbits;
       int64_t maxF = 0;
       for (int64_t f : F) maxF = std::max(maxF, f);
-      maxF = (int64_t)comm->allreduce_max_f64((double)maxF);
       const uint64_t NONE = ~0ull;
+      uint64_t key = 0;
       if (qbits < 63 && (maxF >> (63 - qbits)) == 0) {
-        uint64_t key = NONE;
+        key = NONE;
         for (int64_t i = 0; i < nlocal; ++i)
-          key = std::min(key, ((uint64_t)F[i] << qbits) | (uint64_t)local_to_global[i]);
-        key = comm->allreduce_min_u64(key);
-        if (key == NONE) { minF = -1; minK = -1; }
-        else { minF = (int64_t)(key >> qbits); minK = (int64_t)(key & ((1ull << qbits) - 1)); }
+          key = std::min(key, 1 + (((uint64_t)F[i] << qbits) | (uint64_t)local_to_global[i]));
+      }
+      key = comm->allreduce_min_u64(key);
+      if (key == NONE) { minF = -1; minK = -1; }
+      else if (key != 0) {
+        --key;
+        minF = (int64_t)(key >> qbits);
+        minK = (int64_t)(key & ((1ull << qbits) - 1));
       } else {
         // two-pass fallback when F would not fit next to the query index
         uint64_t mf = NONE;

@@ -212,8 +212,9 @@ def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistC
                   stream=None) -> Tuple[int, int]:
     """Global (minK, minF) with the reference tie-break. (-1, -1) when K == 0 (main.cu:379-380).
 
-    One all-reduce(MIN) of an int64 key F << qbits | q; falls back to two all-reduces when F is
-    too large to share 63 bits with the query index.
+    ONE all-reduce(MIN) of an int64 key 1 + (F << qbits | q). A rank whose F is too large to share
+    62 bits with the query index sends key 0 instead, which every rank then sees as the MIN: all of
+    them take the two-all-reduce fallback together.
     """
     import torch
     import torch.distributed as dist
@@ -222,8 +223,6 @@ def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistC
     idx_local = np.asarray(idx_local, dtype=np.int64)
     qb = _qbits(K)
     NONE = np.iinfo(np.int64).max
-    maxF = int(F_local.max()) if len(F_local) else 0
-    maxF = int(allreduce_max(maxF, ctx)) if ctx.distributed else maxF
     dev = _comm_device(ctx) if ctx.distributed else None
 
     def allmin(v: int) -> int:
@@ -233,11 +232,14 @@ def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistC
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return int(t.item())
 
-    if qb < 63 and (maxF >> (63 - qb)) == 0:
-        keys = (F_local << qb) | idx_local
-        key = allmin(int(keys.min()) if len(keys) else NONE)
-        if key == NONE:
-            return -1, -1
+    maxF = int(F_local.max()) if len(F_local) else 0
+    fits = qb < 62 and (maxF >> (62 - qb)) == 0
+    key = allmin((1 + int(((F_local << qb) | idx_local).min()) if len(F_local) else NONE)
+                 if fits else 0)
+    if key == NONE:
+        return -1, -1
+    if key > 0:
+        key -= 1
         return int(key & ((1 << qb) - 1)), int(key >> qb)
     mf = allmin(int(F_local.min()) if len(F_local) else NONE)
     if mf == NONE:

@@ -69,3 +69,33 @@ def test_packed_argmin_tiebreak_and_fallback():
     big = np.array([2 ** 61, 2 ** 61, 2 ** 62], np.int64)  # too large to pack next to q
     assert D.packed_argmin(big, np.array([7, 3, 1]), 8, ctx) == (3, 2 ** 61)
     assert list(D.round_robin(10, 2, 4)) == [2, 6]
+
+
+def _argmin_worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from msbfs.parallel import distributed as D
+    ctx = D.init_from_env(backend="gloo", use_gpu=False)
+    K = 6
+    F = np.array([9, 4, 2 ** 61, 4, 7, 4], np.int64)  # ties at q = 1, 3, 5
+    res = []
+    for case in ("fit", "mixed", "empty-rank"):
+        idx = D.round_robin(K, rank, world)
+        Fl = F[idx].copy()
+        if case == "fit":
+            Fl[Fl > 100] = 50
+        if case == "empty-rank" and rank == 1:
+            idx, Fl = idx[:0], Fl[:0]
+        res.append(D.packed_argmin(Fl, idx, K, ctx))
+    np.save(os.path.join(out_dir, f"a{rank}.npy"), np.array(res, np.int64))
+    D.shutdown(ctx)
+
+
+def test_packed_argmin_gloo_mixed_fallback(tmp_path):
+    """One rank's F too large to pack: every rank must take the fallback together (one MIN
+    all-reduce decides it) and agree on the reference's lowest-index tie-break."""
+    mp.spawn(_argmin_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        got = [tuple(x) for x in np.load(tmp_path / f"a{r}.npy")]
+        # rank 0 holds q = 0, 2, 4; rank 1 holds q = 1, 3, 5 (round robin)
+        assert got == [(1, 4), (1, 4), (4, 7)], got
