@@ -57,6 +57,7 @@ def main() -> int:
     ap.add_argument("--relabel", type=int, default=1,
                     help="renumber vertices by descending degree after generation (preprocessing)")
     args = ap.parse_args()
+    metric = METRIC if args.scale == 26 else METRIC.replace("RMAT-26", f"RMAT-{args.scale}")
 
     import torch
     import msbfs
@@ -162,7 +163,7 @@ def main() -> int:
     value = total_edges / (ms / 1e3) if ms > 0 else 0.0
     if ctx.rank == 0:
         out = {
-            "metric": METRIC,
+            "metric": metric,
             "value": value,
             "unit": "TEPS",
             "n_gpus": ctx.world,

@@ -328,8 +328,11 @@ int main(int argc, char* argv[]) {
     const int64_t nlocal = (int64_t)local_to_global.size();
     // hybrid exchange buffers: send = own range x all words (destination-major), recv = all
     // vertices x own words
-    DevBuf hsend, hrecv;
-    std::vector<int64_t> scount(P, 0), rcount(P, 0), hout, hF;
+    // zero-word coded exchange (MSBFS_HYB_CODED=0: dense): send/receive coded segments, decode
+    // into hrecv; the phase-A SUM all-reduce also carries the P x P matrix of coded lengths
+    const bool hcoded = !(getenv("MSBFS_HYB_CODED") && atoi(getenv("MSBFS_HYB_CODED")) == 0);
+    DevBuf hsend, hrecv, hrcoded;
+    std::vector<int64_t> scount(P, 0), rcount(P, 0), hout, hF, clen(P, 0);
     const int nw_me = hybrid ? wbeg[me + 1] - wbeg[me] : 0;
     if (hybrid) {
       const int64_t cnt = pcount[me];
@@ -340,9 +343,15 @@ int main(int argc, char* argv[]) {
         ns += scount[j];
         nr += rcount[j];
       }
-      hsend.alloc((size_t)std::max<int64_t>(ns, 1) * 8);
+      int64_t nsc = 0, nrc = 0;
+      for (int j = 0; j < P; ++j) {
+        nsc += hybrid_coded_bound(scount[j]);
+        nrc += hybrid_coded_bound(rcount[j]);
+      }
+      hsend.alloc((size_t)std::max<int64_t>(hcoded ? nsc : ns, 1) * 8);
       hrecv.alloc((size_t)std::max<int64_t>(nr, 1) * 8);
-      hout.resize(2 * K + 3);
+      if (hcoded) hrcoded.alloc((size_t)std::max<int64_t>(nrc, 1) * 8);
+      hout.resize(2 * K + 3 + (hcoded ? (size_t)P * P : 0));
       hF.resize((size_t)std::max(1, 64 * nw_me));
     }
 
@@ -373,12 +382,30 @@ int main(int argc, char* argv[]) {
         // levels 1-2 vertex-partitioned (all groups), one word all-to-all, the rest per rank
         rs = RunStats();
         solver->hybrid_phase_a(K, q.off.data(), q.ids.data(), me, P, n_eff, me == 0, wbeg.data(),
-                               hsend.as<uint64_t>(), hout.data(), &rs, stream);
+                               hsend.as<uint64_t>(), hout.data(), &rs, stream,
+                               hcoded ? clen.data() : nullptr);
         {
           trace::Range range_x("hybrid exchange");
-          comm->alltoallv_device_u64(hsend.as<uint64_t>(), scount, hrecv.as<uint64_t>(), rcount,
-                                     stream);
-          comm->allreduce_sum_i64(hout.data(), hout.size());
+          if (hcoded) {
+            int64_t* M = hout.data() + 2 * K + 3;
+            std::fill(M, M + (size_t)P * P, 0);
+            for (int j = 0; j < P; ++j) M[(size_t)me * P + j] = clen[j];
+            comm->allreduce_sum_i64(hout.data(), hout.size());
+            std::vector<int64_t> sc(P), rc(P);
+            for (int j = 0; j < P; ++j) {
+              sc[j] = M[(size_t)me * P + j];
+              rc[j] = M[(size_t)j * P + me];
+            }
+            comm->alltoallv_device_u64(hsend.as<uint64_t>(), sc, hrcoded.as<uint64_t>(), rc,
+                                       stream);
+            if (nw_me > 0)
+              solver->hybrid_decode(hrcoded.as<uint64_t>(), rc.data(), P, n_eff, nw_me,
+                                    hrecv.as<uint64_t>(), stream);
+          } else {
+            comm->alltoallv_device_u64(hsend.as<uint64_t>(), scount, hrecv.as<uint64_t>(),
+                                       rcount, stream);
+            comm->allreduce_sum_i64(hout.data(), hout.size());
+          }
         }
         solver->hybrid_phase_c(K, wbeg[me], nw_me, P, n_eff, hrecv.as<uint64_t>(), hout.data(),
                                hF.data(), &rs, stream);

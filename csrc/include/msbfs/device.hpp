@@ -143,12 +143,23 @@ class Solver {
   // ceil(K/64)). send_dev: cnt*wbeg[nparts] words, destination-major, cnt = own vertices.
   // out_host[2K+3]: F partial, per-group "new at level 2" flags, then frontier size / edges /
   // visited edges.
+  // coded_len_host != nullptr: send_dev gets the zero-word coded segments instead (see
+  // hybrid_coded_bound / kernels/bitpar.hip "zero-word coding"), coded_len_host[j] = words of
+  // destination j's segment; the segments lie back to back in destination order.
   virtual void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part,
                               int nparts, int64_t n_eff, bool count_l1, const int32_t* wbeg,
                               uint64_t* send_dev, int64_t* out_host, RunStats* st,
-                              hipStream_t stream) {
+                              hipStream_t stream, int64_t* coded_len_host = nullptr) {
     (void)K, (void)qoff, (void)qids, (void)part, (void)nparts, (void)n_eff, (void)count_l1,
-        (void)wbeg, (void)send_dev, (void)out_host, (void)st, (void)stream;
+        (void)wbeg, (void)send_dev, (void)out_host, (void)st, (void)stream, (void)coded_len_host;
+    fail("this solver has no hybrid mode (use the bit-parallel solver)");
+  }
+  // Receiver side of the coded exchange: coded_dev holds one coded segment per source part r
+  // (coded_len_host[r] words each, back to back); dense_dev gets the layout hybrid_phase_c reads.
+  virtual void hybrid_decode(const uint64_t* coded_dev, const int64_t* coded_len_host, int nparts,
+                             int64_t n_eff, int w_count, uint64_t* dense_dev, hipStream_t stream) {
+    (void)coded_dev, (void)coded_len_host, (void)nparts, (void)n_eff, (void)w_count,
+        (void)dense_dev, (void)stream;
     fail("this solver has no hybrid mode (use the bit-parallel solver)");
   }
   // Phase C. recv_dev: for every source part r in order, w_count words of each of r's vertices;
@@ -162,6 +173,9 @@ class Solver {
   }
   SolverOptions opt;
 };
+
+// Largest coded size (words) of a segment of `dense_words` words: every word nonzero.
+inline int64_t hybrid_coded_bound(int64_t dense_words) { return dense_words + (dense_words + 63) / 64; }
 
 // Vertices taking part in the hybrid exchange: 1 + the last vertex with deg > 0 (after degree
 // relabelling every isolated vertex is in the suffix [n_eff, n)).

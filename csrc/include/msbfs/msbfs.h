@@ -130,6 +130,18 @@ int msbfs_solver_hybrid_phase_a(msbfs_solver s, int64_t K, const int64_t* qoff,
                                 const int32_t* qids, int part, int nparts, int64_t n_eff,
                                 int count_l1, const int32_t* wbeg, void* send_dev, int64_t* out,
                                 msbfs_stats* st, void* stream);
+/* Zero-word coded exchange (about half the bytes after level 2): phase_a_coded writes one coded
+ * segment per destination j back to back into send_dev (at most cnt_me*nw_j + ceil(cnt_me*nw_j/64)
+ * u64 each; coded_len[j] = its length, host) and decode expands the received segments (coded_len[r]
+ * u64 from each rank r, in rank order) into the dense recv layout phase_c reads. */
+int msbfs_solver_hybrid_phase_a_coded(msbfs_solver s, int64_t K, const int64_t* qoff,
+                                      const int32_t* qids, int part, int nparts, int64_t n_eff,
+                                      int count_l1, const int32_t* wbeg, void* send_dev,
+                                      int64_t* out, int64_t* coded_len, msbfs_stats* st,
+                                      void* stream);
+int msbfs_solver_hybrid_decode(msbfs_solver s, const void* coded_dev, const int64_t* coded_len,
+                               int nparts, int64_t n_eff, int w_count, void* dense_dev,
+                               void* stream);
 int msbfs_solver_hybrid_phase_c(msbfs_solver s, int64_t K, int w_begin, int w_count, int nparts,
                                 int64_t n_eff, const void* recv_dev, const int64_t* reduced,
                                 int64_t* F_local, msbfs_stats* st, void* stream);

@@ -406,6 +406,32 @@ int msbfs_solver_hybrid_phase_a(msbfs_solver s, int64_t K, const int64_t* qoff,
   });
 }
 
+int msbfs_solver_hybrid_phase_a_coded(msbfs_solver s, int64_t K, const int64_t* qoff,
+                                      const int32_t* qids, int part, int nparts, int64_t n_eff,
+                                      int count_l1, const int32_t* wbeg, void* send_dev,
+                                      int64_t* out, int64_t* coded_len, msbfs_stats* st,
+                                      void* stream) {
+  return guard([&] {
+    if (!coded_len) msbfs::fail("hybrid_phase_a_coded: coded_len is null");
+    timed(s, stream, st, "hybrid phase A", [&](msbfs::RunStats* rs, hipStream_t hs) {
+      s->impl->hybrid_phase_a(K, qoff, qids, part, nparts, n_eff, count_l1 != 0, wbeg,
+                              (uint64_t*)send_dev, out, rs, hs, coded_len);
+    });
+  });
+}
+
+int msbfs_solver_hybrid_decode(msbfs_solver s, const void* coded_dev, const int64_t* coded_len,
+                               int nparts, int64_t n_eff, int w_count, void* dense_dev,
+                               void* stream) {
+  return guard([&] {
+    if (!s || !s->impl) msbfs::fail("null solver");
+    MSBFS_HIP_CHECK(hipSetDevice(s->graph->g.device));
+    msbfs::trace::Range range("hybrid decode");
+    s->impl->hybrid_decode((const uint64_t*)coded_dev, coded_len, nparts, n_eff, w_count,
+                           (uint64_t*)dense_dev, (hipStream_t)stream);
+  });
+}
+
 int msbfs_solver_hybrid_phase_c(msbfs_solver s, int64_t K, int w_begin, int w_count, int nparts,
                                 int64_t n_eff, const void* recv_dev, const int64_t* reduced,
                                 int64_t* F_local, msbfs_stats* st, void* stream) {

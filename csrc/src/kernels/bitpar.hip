@@ -1360,7 +1360,7 @@ template <int W>
 __global__ __launch_bounds__(kBlock, 8) void k_bu_first(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
-    int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF) {
+    int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF, const int32_t* first) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   constexpr int CR = 65;  // bank-skewed counter rows (see BitCounter::spill_strided)
@@ -1389,10 +1389,9 @@ __global__ __launch_bounds__(kBlock, 8) void k_bu_first(
     bool open = false, rnz = false;
     if (valid) {
       v = act[idx];
-      const int64_t b = rowptr[v];
-      deg = (uint32_t)(rowptr[v + 1] - b);
+      const int32_t u = first ? first[v] : col[rowptr[v]];  // active vertices have deg > 0
       r = ldv<VW>(R + (int64_t)v * W + slot * VW);
-      const int32_t u = col[b];  // active vertices have deg > 0
+      deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);  // only counted, off the load chain
       const V<VW> x = ldv<VW>(R + (int64_t)u * W + slot * VW);
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
@@ -1647,6 +1646,18 @@ __global__ __launch_bounds__(kBlock) void k_prefix_lens(const int64_t* rowptr, c
        v += (int64_t)gridDim.x * kBlock) {
     const int64_t b = rowptr[v];
     plen[v] = (int32_t)(row_lower_bound(col, b, rowptr[v + 1], H) - b);
+  }
+}
+
+// first[v] = v's first neighbour (rows sorted: after degree relabelling its biggest hub), -1 for
+// an isolated vertex: the lean first-row pass (k_bu_first) reads it with one coalesced 4-byte load
+// instead of the rowptr -> col chain, whose col[rowptr[v]] touches one 128-byte line per vertex
+__global__ __launch_bounds__(kBlock) void k_first_nbr(const int64_t* rowptr, const int32_t* col,
+                                                      int64_t n, int32_t* first) {
+  for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n;
+       v += (int64_t)gridDim.x * kBlock) {
+    const int64_t b = rowptr[v];
+    first[v] = rowptr[v + 1] > b ? col[b] : -1;
   }
 }
 
@@ -1915,6 +1926,132 @@ __global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, cons
   }
 }
 
+// ---- zero-word coding of the hybrid exchange -------------------------------------------------
+// After level 2 about half of the exchanged 64-bit words are zero (RMAT-26, 1024 groups, 8
+// ranks: 50.5 %). A segment of L words (one destination's share) travels as ceil(L/64) bitmap
+// words (bit i of bitmap word c: word 64c+i is nonzero) followed by its nonzero words in order
+// (parallel/hybrid.py encode_np/decode_np are the reference twins). The sender codes straight
+// from the visited rows (k_code_bits -> scan -> k_code_emit, reading the rows of nonzero words
+// twice instead of writing and re-reading a dense buffer); the receiver expands into the dense
+// layout phase C reads (k_decode_pop -> scan -> k_decode_emit). Chunks (64 words) are numbered
+// globally over the segments; a segment's chunks are [c0[j], c0[j+1]).
+// own vertices of part `part` of `nparts` below n_eff: v = part + i*nparts
+static inline int64_t part_count(int64_t n_eff, int part, int nparts) {
+  return n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
+}
+
+struct CodeSegs {
+  int64_t c0[kMaxParts + 1];  // first global chunk of each segment; c0[nseg] = total chunks
+  int64_t len[kMaxParts];     // dense words of each segment
+  int64_t base[kMaxParts];    // decode: coded start of each segment in the received buffer
+  int64_t dense[kMaxParts];   // decode: dense start of each segment
+};
+
+__device__ __forceinline__ int code_seg(const CodeSegs& cs, int nseg, int64_t c) {
+  int j = 0;
+  while (j + 1 < nseg && c >= cs.c0[j + 1]) ++j;
+  return j;
+}
+
+// word t of destination segment j in k_pack_words' order (0 for deg-0 vertices: stale rows)
+template <int W>
+__device__ __forceinline__ uint64_t code_word(const uint64_t* vis, const int64_t* rowptr, int part,
+                                              int nparts, const WordSplit& ws, int j, int64_t t) {
+  const int nw = ws.b[j + 1] - ws.b[j];
+  const int64_t i = t / nw;
+  const int64_t v = part + i * nparts;
+  if (rowptr[v + 1] == rowptr[v]) return 0ull;
+  return vis[v * W + ws.b[j] + (int)(t - i * nw)];
+}
+
+// one wave per chunk: bitmap word and its popcount
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_code_bits(const uint64_t* vis, const int64_t* rowptr,
+                                                      int part, int nparts, WordSplit ws,
+                                                      CodeSegs cs, int nseg, uint64_t* bits,
+                                                      int64_t* pop) {
+  const int lane = lane_id();
+  const int64_t nch = cs.c0[nseg];
+  for (int64_t c = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; c < nch;
+       c += ((int64_t)gridDim.x * kBlock) >> 6) {
+    const int j = code_seg(cs, nseg, c);
+    const int64_t t = (c - cs.c0[j]) * 64 + lane;
+    const uint64_t x = t < cs.len[j] ? code_word<W>(vis, rowptr, part, nparts, ws, j, t) : 0ull;
+    const uint64_t bm = __ballot(x != 0);
+    if (lane == 0) {
+      bits[c] = bm;
+      pop[c] = __popcll(bm);
+    }
+  }
+}
+
+// incl = inclusive scan of pop. Segment j's coded start is c0[j] + X(c0[j]), X = exclusive
+// prefix: bitmap word of chunk c at c + X(c0[j]), its nonzero words from c0[j+1] + X(c).
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_code_emit(const uint64_t* vis, const int64_t* rowptr,
+                                                      int part, int nparts, WordSplit ws,
+                                                      CodeSegs cs, int nseg, const uint64_t* bits,
+                                                      const int64_t* incl, uint64_t* out) {
+  const int lane = lane_id();
+  const int64_t nch = cs.c0[nseg];
+  for (int64_t c = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; c < nch;
+       c += ((int64_t)gridDim.x * kBlock) >> 6) {
+    const int j = code_seg(cs, nseg, c);
+    const uint64_t bm = bits[c];
+    const int64_t x = incl[c] - __popcll(bm);
+    const int64_t cj = cs.c0[j];
+    if (lane == 0) out[c + incl[cj] - __popcll(bits[cj])] = bm;
+    if ((bm >> lane) & 1ull) {
+      const int64_t t = (c - cj) * 64 + lane;
+      out[cs.c0[j + 1] + x + __popcll(bm & lanemask_lt())] =
+          code_word<W>(vis, rowptr, part, nparts, ws, j, t);
+    }
+  }
+}
+
+// coded length of every segment: its chunks (bitmap words) + its nonzero words
+__global__ void k_code_lens(CodeSegs cs, int nseg, const uint64_t* bits, const int64_t* incl,
+                            int64_t* lens) {
+  const int j = threadIdx.x;
+  if (j >= nseg) return;
+  const int64_t a = cs.c0[j], b = cs.c0[j + 1];
+  lens[j] = b > a ? (b - a) + incl[b - 1] - (incl[a] - __popcll(bits[a])) : 0;
+}
+
+// receiver: one thread per received chunk, popcount of its bitmap word
+__global__ __launch_bounds__(kBlock) void k_decode_pop(const uint64_t* in, CodeSegs cs, int nseg,
+                                                       int64_t* pop) {
+  const int64_t nch = cs.c0[nseg];
+  for (int64_t d = (int64_t)blockIdx.x * kBlock + threadIdx.x; d < nch;
+       d += (int64_t)gridDim.x * kBlock) {
+    const int r = code_seg(cs, nseg, d);
+    pop[d] = __popcll(in[cs.base[r] + (d - cs.c0[r])]);
+  }
+}
+
+// one wave per received chunk: its 64 dense words (zeros included)
+__global__ __launch_bounds__(kBlock) void k_decode_emit(const uint64_t* in, CodeSegs cs, int nseg,
+                                                        const int64_t* incl, uint64_t* dense) {
+  const int lane = lane_id();
+  const int64_t nch = cs.c0[nseg];
+  for (int64_t d = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; d < nch;
+       d += ((int64_t)gridDim.x * kBlock) >> 6) {
+    const int r = code_seg(cs, nseg, d);
+    const int64_t d0 = cs.c0[r], q = d - d0;
+    const uint64_t* seg = in + cs.base[r];
+    const uint64_t bm = seg[q];
+    // nonzero words before this chunk in segment r
+    const int64_t before = (incl[d] - __popcll(bm)) - (incl[d0] - __popcll(seg[0]));
+    const int64_t t = q * 64 + lane;
+    if (t < cs.len[r]) {
+      uint64_t x = 0;
+      if ((bm >> lane) & 1ull)
+        x = seg[(cs.c0[r + 1] - d0) + before + __popcll(bm & lanemask_lt())];
+      dense[cs.dense[r] + t] = x;
+    }
+  }
+}
+
 // Phase C state from the received words: both visited buffers (stride W, zero padding beyond
 // nw), done = every alive group present, anyvis = any bit. One thread per vertex; the bitmaps
 // are written with plain stores from wave ballots (64 vertices = 2 words), so no memset.
@@ -2077,6 +2214,8 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_CODES")) codes_ = atoi(x);
     if (const char* x = getenv("MSBFS_LEAN")) lean_ = atoi(x);
     if (const char* x = getenv("MSBFS_LEAN_MIN")) lean_min_ = atoll(x);
+    if (const char* x = getenv("MSBFS_LEAN_LEVEL")) lean_level_ = atoi(x);
+    if (const char* x = getenv("MSBFS_FIRST")) first_on_ = atoi(x);
 
     if (const char* x = getenv("MSBFS_HUBBIG")) hub_big_ = atoi(x);
     if (const char* x = getenv("MSBFS_PFX")) pfx_ = atoi(x);
@@ -2118,7 +2257,8 @@ class BitparSolver final : public Solver {
 
   void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,
                       int64_t n_eff, bool count_l1, const int32_t* wbeg, uint64_t* send,
-                      int64_t* out, RunStats* st, hipStream_t s) override {
+                      int64_t* out, RunStats* st, hipStream_t s,
+                      int64_t* coded_len = nullptr) override {
     if (K < 1 || K > hybrid_max_groups())
       fail("hybrid mode: K=" + std::to_string(K) + " groups exceeds one round (" +
            std::to_string(hybrid_max_groups()) + ")");
@@ -2133,7 +2273,8 @@ class BitparSolver final : public Solver {
     while (w < wt) w <<= 1;
 #define MSBFS_BP_CASE(WW)                                                                  \
   case WW:                                                                                 \
-    phase_a_impl<WW>(K, qoff, qids, part, nparts, n_eff, count_l1, wbeg, send, out, st, s); \
+    phase_a_impl<WW>(K, qoff, qids, part, nparts, n_eff, count_l1, wbeg, send, out, st, s, \
+                     coded_len);                                                             \
     break;
     switch (w) {
       MSBFS_BP_CASE(1)
@@ -2237,7 +2378,8 @@ class BitparSolver final : public Solver {
   template <int W>
   void phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,
                     int64_t n_eff, bool count_l1, const int32_t* wbeg, uint64_t* send,
-                    int64_t* out, RunStats* st, hipStream_t s);
+                    int64_t* out, RunStats* st, hipStream_t s,
+                    int64_t* coded_len);
   template <int W>
   void phase_c_impl(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
                     const uint64_t* recv, const int64_t* reduced, int64_t* F_out, RunStats* st,
@@ -2291,6 +2433,107 @@ class BitparSolver final : public Solver {
     return plen_.as<int32_t>();
   }
 
+  // scratch of the exchange coding: bitmap words, popcounts and their inclusive scan per chunk
+  struct CodeWs {
+    uint64_t* bits;
+    int64_t* pop;
+    int64_t* incl;
+    void* tmp;
+    size_t tmp_bytes;
+  };
+  CodeWs code_ws(int64_t chunks) {
+    const size_t a = ((size_t)chunks * 8 + 255) & ~size_t(255);
+    const size_t tb = inclusive_scan_temp_bytes(chunks);
+    code_ws_.ensure(3 * a + tb);
+    char* p = (char*)code_ws_.p;
+    return CodeWs{(uint64_t*)p, (int64_t*)(p + a), (int64_t*)(p + 2 * a), p + 3 * a, tb};
+  }
+
+  // zero-word coded send segments of phase A (see k_code_bits); coded_len[j] (host) = words of
+  // destination j's segment
+  template <int W>
+  void code_send(const uint64_t* vis, int64_t cnt, int part, int nparts, const WordSplit& ws,
+                 uint64_t* send, int64_t* coded_len, hipStream_t s) {
+    CodeSegs cs{};
+    int64_t c = 0;
+    for (int j = 0; j < nparts; ++j) {
+      cs.c0[j] = c;
+      cs.len[j] = cnt * (ws.b[j + 1] - ws.b[j]);
+      c += (cs.len[j] + 63) / 64;
+    }
+    cs.c0[nparts] = c;
+    for (int j = 0; j < nparts; ++j) coded_len[j] = 0;
+    if (c == 0) return;
+    const CodeWs w = code_ws(c);
+    k_code_bits<W><<<grid_for(c * 64, kBlock, 8192), kBlock, 0, s>>>(
+        vis, g_.rowptr, part, nparts, ws, cs, nparts, w.bits, w.pop);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    inclusive_scan_i64(w.pop, w.incl, c, w.tmp, w.tmp_bytes, s);
+    k_code_emit<W><<<grid_for(c * 64, kBlock, 8192), kBlock, 0, s>>>(
+        vis, g_.rowptr, part, nparts, ws, cs, nparts, w.bits, w.incl, send);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    k_code_lens<<<1, 64, 0, s>>>(cs, nparts, w.bits, w.incl, w.pop);  // pop is free again
+    MSBFS_HIP_CHECK(hipGetLastError());
+    MSBFS_HIP_CHECK(hipMemcpyAsync(coded_len, w.pop, nparts * sizeof(int64_t),
+                                   hipMemcpyDeviceToHost, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+
+  void hybrid_decode(const uint64_t* coded, const int64_t* coded_len, int nparts, int64_t n_eff,
+                     int w_count, uint64_t* dense, hipStream_t s) override {
+    if (nparts < 1 || nparts > kMaxParts) fail("hybrid mode: 1..64 ranks");
+    if (w_count < 0 || w_count > maxW_) fail("hybrid mode: bad word block");
+    CodeSegs cs{};
+    int64_t c = 0, base = 0, dn = 0;
+    for (int r = 0; r < nparts; ++r) {
+      const int64_t L = part_count(n_eff, r, nparts) * w_count, nch = (L + 63) / 64;
+      if (coded_len[r] < nch || coded_len[r] > L + nch)
+        fail("hybrid decode: coded segment " + std::to_string(r) + " has " +
+             std::to_string(coded_len[r]) + " words, outside [" + std::to_string(nch) + ", " +
+             std::to_string(L + nch) + "]");
+      cs.c0[r] = c;
+      cs.len[r] = L;
+      cs.base[r] = base;
+      cs.dense[r] = dn;
+      c += nch;
+      base += coded_len[r];
+      dn += L;
+    }
+    cs.c0[nparts] = c;
+    if (c == 0) return;
+    const CodeWs w = code_ws(c);
+    k_decode_pop<<<grid_for(c, kBlock, 8192), kBlock, 0, s>>>(coded, cs, nparts, w.pop);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    inclusive_scan_i64(w.pop, w.incl, c, w.tmp, w.tmp_bytes, s);
+    k_decode_emit<<<grid_for(c * 64, kBlock, 8192), kBlock, 0, s>>>(coded, cs, nparts, w.incl,
+                                                                     dense);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+
+  // first[v] for every vertex (cached per graph buffers like prefix_lens); nullptr when the
+  // 4n bytes do not fit comfortably (RMAT-30) or MSBFS_FIRST=0: k_bu_first then reads col
+  const int32_t* first_nbr(hipStream_t s) {
+    if (!first_on_) return nullptr;
+    if (first_key_[0] != (const void*)g_.rowptr || first_key_[1] != (const void*)g_.col) {
+      const size_t bytes = (size_t)std::max<int64_t>(g_.n, 1) * sizeof(int32_t);
+      if (first_.bytes < bytes) {
+        size_t fr = 0, tot = 0;
+        MSBFS_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+        if (fr < bytes + ((size_t)2 << 30)) {
+          first_on_ = 0;
+          return nullptr;
+        }
+      }
+      first_.ensure(bytes);
+      k_first_nbr<<<grid_for(g_.n, kBlock, 8192), kBlock, 0, s>>>(g_.rowptr, g_.col, g_.n,
+                                                                   first_.as<int32_t>());
+      MSBFS_HIP_CHECK(hipGetLastError());
+      first_key_[0] = g_.rowptr;
+      first_key_[1] = g_.col;
+    }
+    return first_.as<int32_t>();
+  }
+
   HostCtr read_ctr(hipStream_t s) {
     MSBFS_HIP_CHECK(hipMemcpyAsync(hctr_->p, ctr_.p, sizeof(Ctr), hipMemcpyDeviceToHost, s));
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
@@ -2329,7 +2572,12 @@ class BitparSolver final : public Solver {
   // row); on the second pull level most vertices overflow (128 groups: level 3 3.5 -> 4.1 ms)
   int lean_ = 1;
   int64_t lean_min_ = 1 << 20;  // MSBFS_LEAN_MIN: smallest active list for the lean pass
+  int lean_level_ = 3;          // MSBFS_LEAN_LEVEL: first pull level (1-based) that may run it
   DevBuf plen_;
+  DevBuf first_;
+  DevBuf code_ws_;
+  const void* first_key_[2] = {nullptr, nullptr};
+  int first_on_ = 1;  // MSBFS_FIRST=0: no first-neighbour array (A/B knob)
   const void* plen_key_[2] = {nullptr, nullptr};
   int32_t plen_h_ = 0;
   // MSBFS_PFX: 0 = the first bottom-up level pulls whole rows (no tail push); 1 = prefix bound at
@@ -2709,14 +2957,15 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
           // 4 3.1 -> 2.5 ms; level 3 prefers full steps: 6.5 vs 6.7 ms). MSBFS_NARROW_C: 0 off,
           // 1 always, 2 (default) this rule
           const bool short1 = narrow_c_ == 1 || (narrow_c_ == 2 && (S.bu_levels >= 3 || W <= 4));
-          if (lean_ && !S.lean_off && fuse && !filt && S.bu_levels >= 3 && S.nact >= lean_min_) {
+          if (lean_ && !S.lean_off && fuse && !filt && S.bu_levels >= lean_level_ &&
+              S.nact >= lean_min_) {
             S.lean_ran = true;
             // lean first pass, then the regular pull over the vertices it could not finish
             const int gl = grid_for(S.nact, L::TILE, grid);
             k_bu_first<W><<<gl, kBlock, 0, s>>>(
                 act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
                 done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-                ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF(rows));
+                ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF(rows), first_nbr(s));
             MSBFS_HIP_CHECK(hipGetLastError());
             rows += gl;
             k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
@@ -3044,17 +3293,13 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
   }
 }
 
-// own vertices of part `part` of `nparts` below n_eff: v = part + i*nparts
-static inline int64_t part_count(int64_t n_eff, int part, int nparts) {
-  return n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
-}
-
 // Phase A: level 1 (top-down, every rank identical, only rank 0 adds it to F), level 2
 // (bottom-up over this rank's residue class only), then pack its rows' words per destination.
 template <int W>
 void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int part,
                                 int nparts, int64_t n_eff, bool count_l1, const int32_t* wbeg,
-                                uint64_t* send, int64_t* out, RunStats* st, hipStream_t s) {
+                                uint64_t* send, int64_t* out, RunStats* st, hipStream_t s,
+                                int64_t* coded_len) {
   Loop S;
   S.part = part;
   S.nparts = nparts;
@@ -3071,10 +3316,12 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   const int wt = (int)((K + 63) / 64);
-  if (S.cnt > 0) {
-    WordSplit ws{};
-    for (int j = 0; j <= nparts; ++j) ws.b[j] = wbeg[j];
-    for (int j = nparts + 1; j <= kMaxParts; ++j) ws.b[j] = wt + 1;  // never reached
+  WordSplit ws{};
+  for (int j = 0; j <= nparts; ++j) ws.b[j] = wbeg[j];
+  for (int j = nparts + 1; j <= kMaxParts; ++j) ws.b[j] = wt + 1;  // never reached
+  if (coded_len) {
+    code_send<W>(vis_[S.cur].as<uint64_t>(), S.cnt, part, nparts, ws, send, coded_len, s);
+  } else if (S.cnt > 0) {
     k_pack_words<W><<<grid_for(S.cnt * wt, kBlock, 8192), kBlock, 0, s>>>(
         vis_[S.cur].as<uint64_t>(), g_.rowptr, part, nparts, S.cnt, wt, ws, send);
     MSBFS_HIP_CHECK(hipGetLastError());

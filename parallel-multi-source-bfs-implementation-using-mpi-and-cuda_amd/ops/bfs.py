@@ -81,20 +81,37 @@ class Solver:
 
     def hybrid_phase_a(self, queries: QuerySet, part: int, nparts: int, n_eff: int,
                        count_l1: bool, wbeg: np.ndarray, send_ptr: int,
-                       stream: Optional[int] = None):
+                       stream: Optional[int] = None, coded: bool = False):
         """Levels 1-2 of all groups, level-2 pulls only for the vertices v = part + i*nparts
         below n_eff; packs their visited words into the device buffer at send_ptr (destination-
-        major). Returns (out[2K+3], stats)."""
+        major). Returns (out[2K+3], stats). coded: the send buffer gets one zero-word coded
+        segment per destination instead (hybrid.encode_np), stats["coded_len"] their lengths."""
         K = queries.K
         wbeg = np.ascontiguousarray(wbeg, dtype=np.int32)
         out = np.zeros(2 * K + 3, dtype=np.int64)
         st = native.Stats()
-        native.check(native.lib().msbfs_solver_hybrid_phase_a(
-            self._h, K, native.ptr(queries.off, C.c_int64), native.ptr(queries.ids, C.c_int32),
-            int(part), int(nparts), int(n_eff), int(bool(count_l1)), native.ptr(wbeg, C.c_int32),
-            C.c_void_p(send_ptr), native.ptr(out, C.c_int64), C.byref(st),
-            C.c_void_p(stream) if stream else None))
+        args = (self._h, K, native.ptr(queries.off, C.c_int64), native.ptr(queries.ids, C.c_int32),
+                int(part), int(nparts), int(n_eff), int(bool(count_l1)),
+                native.ptr(wbeg, C.c_int32), C.c_void_p(send_ptr), native.ptr(out, C.c_int64))
+        strm = C.c_void_p(stream) if stream else None
+        if coded:
+            lens = np.zeros(int(nparts), dtype=np.int64)
+            native.check(native.lib().msbfs_solver_hybrid_phase_a_coded(
+                *args, native.ptr(lens, C.c_int64), C.byref(st), strm))
+            d = st.as_dict()
+            d["coded_len"] = lens
+            return out, d
+        native.check(native.lib().msbfs_solver_hybrid_phase_a(*args, C.byref(st), strm))
         return out, st.as_dict()
+
+    def hybrid_decode(self, coded_ptr: int, coded_len: np.ndarray, nparts: int, n_eff: int,
+                      w_count: int, dense_ptr: int, stream: Optional[int] = None) -> None:
+        """Expand the received coded segments (coded_len[r] u64 from each part r, back to back)
+        into the dense layout hybrid_phase_c reads (asynchronous on the solver's stream)."""
+        lens = np.ascontiguousarray(coded_len, dtype=np.int64)
+        native.check(native.lib().msbfs_solver_hybrid_decode(
+            self._h, C.c_void_p(coded_ptr), native.ptr(lens, C.c_int64), int(nparts), int(n_eff),
+            int(w_count), C.c_void_p(dense_ptr), C.c_void_p(stream) if stream else None))
 
     def hybrid_phase_c(self, K: int, w_begin: int, w_count: int, nparts: int, n_eff: int,
                        recv_ptr: int, reduced: np.ndarray, stream: Optional[int] = None):

@@ -107,6 +107,11 @@ def _sig(lib):
         "msbfs_solver_hybrid_phase_a": (C.c_int, [vp, C.c_int64, i64p, i32p, C.c_int, C.c_int,
                                                   C.c_int64, C.c_int, i32p, vp, i64p, P(Stats),
                                                   vp]),
+        "msbfs_solver_hybrid_phase_a_coded": (C.c_int, [vp, C.c_int64, i64p, i32p, C.c_int,
+                                                        C.c_int, C.c_int64, C.c_int, i32p, vp,
+                                                        i64p, i64p, P(Stats), vp]),
+        "msbfs_solver_hybrid_decode": (C.c_int, [vp, vp, i64p, C.c_int, C.c_int64, C.c_int, vp,
+                                                 vp]),
         "msbfs_solver_hybrid_phase_c": (C.c_int, [vp, C.c_int64, C.c_int, C.c_int, C.c_int,
                                                   C.c_int64, vp, i64p, i64p, P(Stats), vp]),
     }

@@ -14,7 +14,11 @@ keeps the replica but changes the split:
            n_eff (= 1 + the last vertex with an edge; a degree-relabelled graph keeps its
            isolated vertices in the suffix, which is never sent), the words of its own group
            block (1/N of the words); plus one small SUM all-reduce of the phase-A partial sums,
-           "still alive" flags and frontier sizes.
+           "still alive" flags and frontier sizes. About half of those words are zero after
+           level 2 (RMAT-26, 1024 groups, 8 ranks: 50.5 %), so each destination's share travels
+           zero-word coded (encode_np: a bitmap word per 64 words + the nonzero words; the
+           same all-reduce carries the N x N matrix of coded lengths) and the receiver expands
+           it on the GPU (Solver.hybrid_decode).
   phase C  every rank continues its own groups from level 3 (bit-parallel, as in round-robin).
 
 Result: F[k] = reduced[k] + F_C[k] for the own groups; the global argmin is the usual 8-byte
@@ -25,6 +29,7 @@ exchange moves whole words.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
+import os
 from typing import Optional
 
 import numpy as np
@@ -62,6 +67,42 @@ def split_sizes(n_eff: int, wbeg: np.ndarray, rank: int):
     send = [cnt * int(wbeg[j + 1] - wbeg[j]) for j in range(world)]
     recv = [part_count(n_eff, r, world) * nw_me for r in range(world)]
     return send, recv
+
+
+def coded_bound(words: int) -> int:
+    """Largest zero-word coded size of a segment of `words` words (all nonzero)."""
+    return int(words) + (int(words) + 63) // 64
+
+
+def coding_default() -> bool:
+    """Zero-word coded exchange unless MSBFS_HYB_CODED=0 (A/B knob)."""
+    return os.environ.get("MSBFS_HYB_CODED", "1") != "0"
+
+
+def encode_np(words: np.ndarray) -> np.ndarray:
+    """Twin of k_code_bits/k_code_emit for one segment: ceil(L/64) bitmap words (bit i of word c
+    set iff words[64c+i] != 0), then the nonzero words in order."""
+    words = np.asarray(words, dtype=np.uint64)
+    L = len(words)
+    nch = (L + 63) // 64
+    nz = np.zeros(nch * 64, dtype=bool)
+    nz[:L] = words != 0
+    bm = (nz.reshape(nch, 64).astype(np.uint64) << np.arange(64, dtype=np.uint64)).sum(
+        axis=1, dtype=np.uint64)
+    return np.concatenate([bm, words[nz[:L]]])
+
+
+def decode_np(coded: np.ndarray, L: int) -> np.ndarray:
+    """Twin of k_decode_pop/k_decode_emit: one coded segment back to its L dense words."""
+    coded = np.asarray(coded, dtype=np.uint64)
+    nch = (L + 63) // 64
+    bits = ((coded[:nch, None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(bool)
+    bits = bits.reshape(-1)[:L]
+    if len(coded) != nch + int(bits.sum()):
+        raise ValueError(f"coded segment has {len(coded)} words, expected {nch + int(bits.sum())}")
+    out = np.zeros(L, dtype=np.uint64)
+    out[bits] = coded[nch:]
+    return out
 
 
 # ---- numpy emulation of the device layout (tests; documents the kernels' contract) ----------
@@ -109,7 +150,7 @@ class HybridResult:
 class HybridRunner:
     """Reusable buffers + plan for one (solver, K, world) combination."""
 
-    def __init__(self, solver, K: int, ctx: D.DistContext):
+    def __init__(self, solver, K: int, ctx: D.DistContext, coded: Optional[bool] = None):
         import torch
 
         self.solver, self.K, self.ctx = solver, int(K), ctx
@@ -119,57 +160,82 @@ class HybridRunner:
                              f"round, got {self.K}")
         if ctx.world > MAX_PARTS:
             raise ValueError(f"hybrid mode handles at most {MAX_PARTS} ranks, got {ctx.world}")
+        self.coded = coding_default() if coded is None else bool(coded)
         self.n_eff = g.hybrid_extent()
         self.wbeg = word_split(self.K, ctx.world)
         self.idx = own_groups(self.K, self.wbeg, ctx.rank)
         self.send_sizes, self.recv_sizes = split_sizes(self.n_eff, self.wbeg, ctx.rank)
         self.nw = int(self.wbeg[ctx.rank + 1] - self.wbeg[ctx.rank])
         dev = torch.device("cuda", g.device)
-        self.send = torch.empty(max(1, sum(self.send_sizes)), dtype=torch.int64, device=dev)
+        ns = sum(coded_bound(x) for x in self.send_sizes) if self.coded else sum(self.send_sizes)
+        self.send = torch.empty(max(1, ns), dtype=torch.int64, device=dev)
         self.recv = torch.empty(max(1, sum(self.recv_sizes)), dtype=torch.int64, device=dev)
+        self.rcoded = (torch.empty(max(1, sum(coded_bound(x) for x in self.recv_sizes)),
+                                   dtype=torch.int64, device=dev) if self.coded else None)
         self._staged = ctx.distributed and ctx.backend != "nccl"
+        self.last_bytes = (0, 0)  # (sent, received) of the last exchange
 
-    def _exchange(self, out: np.ndarray) -> np.ndarray:
+    def _all_to_all(self, recv, send, rsz, ssz) -> None:
         import torch
         import torch.distributed as dist
 
-        ctx = self.ctx
-        if not ctx.distributed:
-            self.recv[:sum(self.recv_sizes)].copy_(self.send[:sum(self.send_sizes)])
-            return out
-        if self._staged:  # gloo: through host memory
-            s = self.send[:sum(self.send_sizes)].cpu()
-            r = torch.empty(sum(self.recv_sizes), dtype=torch.int64)
-            dist.all_to_all_single(r, s, self.recv_sizes, self.send_sizes)
-            self.recv[:sum(self.recv_sizes)].copy_(r)
-            t = torch.from_numpy(out)
+        if not self.ctx.distributed:
+            recv[:sum(rsz)].copy_(send[:sum(ssz)])
+        elif self._staged:  # gloo: through host memory
+            s = send[:sum(ssz)].cpu()
+            r = torch.empty(sum(rsz), dtype=torch.int64)
+            dist.all_to_all_single(r, s, list(rsz), list(ssz))
+            recv[:sum(rsz)].copy_(r)
         else:
-            dist.all_to_all_single(self.recv[:sum(self.recv_sizes)],
-                                   self.send[:sum(self.send_sizes)],
-                                   self.recv_sizes, self.send_sizes)
-            t = torch.from_numpy(out).to(self.send.device)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        res = t.cpu().numpy()
+            dist.all_to_all_single(recv[:sum(rsz)], send[:sum(ssz)], list(rsz), list(ssz))
+        if self.ctx.distributed or recv.is_cuda:
+            # the native kernels run on their own stream: make the received words visible first
+            torch.cuda.current_stream(recv.device).synchronize()
+
+    def _allreduce(self, vec: np.ndarray) -> np.ndarray:
+        import torch
+        import torch.distributed as dist
+
+        if not self.ctx.distributed:
+            return vec
+        t = torch.from_numpy(vec)
         if not self._staged:
-            # the native phase C runs on its own stream: make the received words visible first
-            torch.cuda.current_stream(self.send.device).synchronize()
-        return res
+            t = t.to(self.send.device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.cpu().numpy()
 
     def run(self, queries) -> HybridResult:
         if queries.K != self.K:
             raise ValueError("query count differs from the plan")
-        ctx = self.ctx
-        out, sa = self.solver.hybrid_phase_a(queries, ctx.rank, ctx.world, self.n_eff,
-                                             ctx.rank == 0, self.wbeg, self.send.data_ptr())
-        reduced = self._exchange(out)
-        Fc, sc = self.solver.hybrid_phase_c(self.K, int(self.wbeg[ctx.rank]), self.nw, ctx.world,
+        ctx, P = self.ctx, self.ctx.world
+        out, sa = self.solver.hybrid_phase_a(queries, ctx.rank, P, self.n_eff, ctx.rank == 0,
+                                             self.wbeg, self.send.data_ptr(), coded=self.coded)
+        if self.coded:
+            # one SUM all-reduce: phase-A partial sums + the P x P matrix of coded lengths
+            ext = np.zeros(len(out) + P * P, dtype=np.int64)
+            ext[:len(out)] = out
+            ext[len(out) + ctx.rank * P:len(out) + (ctx.rank + 1) * P] = sa["coded_len"]
+            ext = self._allreduce(ext)
+            reduced = ext[:len(out)]
+            M = ext[len(out):].reshape(P, P)
+            ssz, rsz = [int(x) for x in M[ctx.rank]], [int(x) for x in M[:, ctx.rank]]
+            self._all_to_all(self.rcoded, self.send, rsz, ssz)
+            self.solver.hybrid_decode(self.rcoded.data_ptr(), np.array(rsz, np.int64), P,
+                                      self.n_eff, self.nw, self.recv.data_ptr())
+        else:
+            ssz, rsz = self.send_sizes, self.recv_sizes
+            reduced = self._allreduce(out.copy())
+            self._all_to_all(self.recv, self.send, rsz, ssz)
+        self.last_bytes = (8 * sum(ssz), 8 * sum(rsz))
+        Fc, sc = self.solver.hybrid_phase_c(self.K, int(self.wbeg[ctx.rank]), self.nw, P,
                                             self.n_eff, self.recv.data_ptr(), reduced)
         F = reduced[self.idx] + Fc[:len(self.idx)]
         stats = {"levels": sa.get("levels", 0) + sc.get("levels", 0),
                  "td_levels": sa.get("td_levels", 0) + sc.get("td_levels", 0),
                  "bu_levels": sa.get("bu_levels", 0) + sc.get("bu_levels", 0),
                  "phase_a_ms": sa.get("device_ms"), "phase_c_ms": sc.get("device_ms"),
-                 "part": (ctx.rank, ctx.world, self.n_eff), "words": self.nw}
+                 "part": (ctx.rank, P, self.n_eff), "words": self.nw,
+                 "sent_bytes": self.last_bytes[0], "coded": self.coded}
         return HybridResult(self.idx, F, stats)
 
 
@@ -179,37 +245,67 @@ def hybrid_bfs(solver, queries, ctx: Optional[D.DistContext] = None) -> HybridRe
     return HybridRunner(solver, queries.K, ctx).run(queries)
 
 
-def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None) -> np.ndarray:
+def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
+                  coded: Optional[bool] = None) -> np.ndarray:
     """Run the hybrid algorithm for `world` ranks sequentially in ONE process on one GPU (no
     torch.distributed): phase A of every rank, a host-side all-to-all, phase C of every rank.
     Returns the full F vector. Used by the GPU tests and to time per-rank phases: with
-    `timings` (a list) one dict per rank is appended (phase A / C device ms, send/recv bytes)."""
+    `timings` (a list) one dict per rank is appended (phase A / C device ms, send/recv bytes).
+    coded: zero-word coded exchange (default: coding_default()), decoded on the GPU."""
     import torch
 
+    coded = coding_default() if coded is None else bool(coded)
     K = queries.K
     g = solver.graph
     n_eff = g.hybrid_extent()
     wbeg = word_split(K, world)
     dev = torch.device("cuda", g.device)
-    sends, outs = [], []
+    sends, outs, lens = [], [], []
     for r in range(world):
         ss, rs = split_sizes(n_eff, wbeg, r)
-        buf = torch.empty(max(1, sum(ss)), dtype=torch.int64, device=dev)
-        out, sa = solver.hybrid_phase_a(queries, r, world, n_eff, r == 0, wbeg, buf.data_ptr())
-        if timings is not None:
-            timings.append({"rank": r, "vertices": part_count(n_eff, r, world),
-                            "phase_a_ms": sa["device_ms"], "send_bytes": 8 * sum(ss),
-                            "recv_bytes": 8 * sum(rs), "phase_c_ms": 0.0})
-        sends.append(buf[:sum(ss)].cpu().numpy().view(np.uint64))
+        nb = sum(coded_bound(x) for x in ss) if coded else sum(ss)
+        buf = torch.empty(max(1, nb), dtype=torch.int64, device=dev)
+        out, sa = solver.hybrid_phase_a(queries, r, world, n_eff, r == 0, wbeg, buf.data_ptr(),
+                                        coded=coded)
+        cl = [int(x) for x in sa["coded_len"]] if coded else list(ss)
+        dense = buf[:sum(ss)].cpu().numpy().view(np.uint64) if not coded else None
+        sends.append(buf[:sum(cl)].cpu().numpy().view(np.uint64))
+        lens.append(cl)
         outs.append(out)
+        if timings is not None:
+            if coded:  # how much the coding saved: the dense twin of this rank's segments
+                offs = np.concatenate([[0], np.cumsum(cl)])
+                zero = sum(int(len(x) - np.count_nonzero(x)) for x in
+                           (decode_np(sends[-1][offs[j]:offs[j + 1]], ss[j]) for j in range(world)))
+            else:
+                zero = int(len(dense) - np.count_nonzero(dense))
+            timings.append({"rank": r, "vertices": part_count(n_eff, r, world),
+                            "phase_a_ms": sa["device_ms"], "send_bytes": 8 * sum(cl),
+                            "dense_send_bytes": 8 * sum(ss), "recv_bytes": 0,
+                            "send_zero_frac": zero / max(1, sum(ss)), "phase_c_ms": 0.0})
     reduced = np.sum(outs, axis=0)
-    recvs = all_to_all_np(sends, n_eff, wbeg)
     F = np.zeros(K, dtype=np.int64)
     for j in range(world):
         nw = int(wbeg[j + 1] - wbeg[j])
+        rsz = [lens[r][j] for r in range(world)]
+        parts = []
+        for r in range(world):
+            o = sum(lens[r][:j])
+            parts.append(sends[r][o:o + lens[r][j]])
+        rbuf = np.concatenate(parts) if parts else np.zeros(0, np.uint64)
+        if timings is not None:
+            timings[len(timings) - world + j]["recv_bytes"] = 8 * len(rbuf)
         if nw == 0:
             continue
-        rt = torch.from_numpy(recvs[j].view(np.int64)).to(dev)
+        rt = torch.from_numpy(rbuf.view(np.int64)).to(dev) if len(rbuf) else \
+            torch.zeros(1, dtype=torch.int64, device=dev)
+        if coded:
+            dense = torch.empty(max(1, sum(split_sizes(n_eff, wbeg, j)[1])), dtype=torch.int64,
+                                device=dev)
+            torch.cuda.synchronize(dev)
+            solver.hybrid_decode(rt.data_ptr(), np.array(rsz, np.int64), world, n_eff, nw,
+                                 dense.data_ptr())
+            rt = dense
         Fc, sc = solver.hybrid_phase_c(K, int(wbeg[j]), nw, world, n_eff, rt.data_ptr(), reduced)
         if timings is not None:
             timings[len(timings) - world + j]["phase_c_ms"] = sc["device_ms"]

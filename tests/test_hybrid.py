@@ -94,6 +94,84 @@ def test_gloo_all_to_all_matches_emulation(tmp_path, world):
         assert np.array_equal(H.unpack_np(got, n, n_eff, world, nw), want)
 
 
+def test_word_codec_roundtrip():
+    """Zero-word coding of one exchange segment: bitmap words + nonzero words, exact round trip,
+    never larger than coded_bound (the buffer size the runner allocates)."""
+    H = _H()
+    rng = np.random.default_rng(1)
+    for L in (0, 1, 5, 63, 64, 65, 127, 128, 129, 1000):
+        for dens in (0.0, 0.02, 0.5, 1.0):
+            w = rng.integers(1, 2**64 - 1, size=L, dtype=np.uint64, endpoint=True)
+            w[rng.random(L) >= dens] = 0
+            c = H.encode_np(w)
+            nch = (L + 63) // 64
+            assert len(c) == nch + np.count_nonzero(w) <= H.coded_bound(L)
+            assert np.array_equal(H.decode_np(c, L), w)
+    # the bitmap is little-endian within a word: word 64c + i -> bit i of bitmap word c
+    w = np.zeros(70, np.uint64)
+    w[[0, 63, 64, 69]] = [5, 6, 7, 8]
+    c = H.encode_np(w)
+    assert int(c[0]) == (1 | (1 << 63)) and int(c[1]) == (1 | (1 << 5))
+    assert list(c[2:]) == [5, 6, 7, 8]
+    with pytest.raises(ValueError):
+        H.decode_np(c[:-1], 70)
+
+
+def _coded_worker(rank, world, port, out_dir):
+    """The runner's coded protocol over gloo with numpy twins of the kernels: one SUM all-reduce
+    of the coded-length matrix, an all-to-all of the coded segments, per-source decode."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from msbfs.parallel import distributed as D
+    from msbfs.parallel import hybrid as H
+    ctx = D.init_from_env(backend="gloo", use_gpu=False)
+    K, n, n_eff = 700, 301, 290
+    wbeg = H.word_split(K, world)
+    rng = np.random.default_rng(9)
+    vis = rng.integers(0, 2**62, size=(n, 16), dtype=np.uint64)
+    vis[rng.random((n, 16)) < 0.6] = 0
+    dense = H.pack_words_np(vis, rank, world, n_eff, wbeg)
+    ss, rs = H.split_sizes(n_eff, wbeg, rank)
+    offs = np.concatenate([[0], np.cumsum(ss)])
+    segs = [H.encode_np(dense[offs[j]:offs[j + 1]]) for j in range(world)]
+    M = np.zeros((world, world), np.int64)
+    M[rank] = [len(x) for x in segs]
+    t = torch.from_numpy(M.reshape(-1))
+    dist.all_reduce(t)
+    M = t.numpy().reshape(world, world)
+    ssz, rsz = [int(x) for x in M[rank]], [int(x) for x in M[:, rank]]
+    r = torch.empty(sum(rsz), dtype=torch.int64)
+    dist.all_to_all_single(r, torch.from_numpy(np.concatenate(segs).view(np.int64)), rsz, ssz)
+    got, o = [], 0
+    for src in range(world):
+        got.append(H.decode_np(r.numpy()[o:o + rsz[src]].view(np.uint64), rs[src]))
+        o += rsz[src]
+    np.save(os.path.join(out_dir, f"c{rank}.npy"), np.concatenate(got))
+    np.save(os.path.join(out_dir, f"b{rank}.npy"), np.array([sum(ssz), sum(ss)]))
+    D.shutdown(ctx)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_coded_exchange(tmp_path, world):
+    H = _H()
+    mp.spawn(_coded_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    K, n, n_eff = 700, 301, 290
+    wbeg = H.word_split(K, world)
+    rng = np.random.default_rng(9)
+    vis = rng.integers(0, 2**62, size=(n, 16), dtype=np.uint64)
+    vis[rng.random((n, 16)) < 0.6] = 0
+    for j in range(world):
+        nw = int(wbeg[j + 1] - wbeg[j])
+        got = np.load(tmp_path / f"c{j}.npy")
+        want = vis[:, wbeg[j]:wbeg[j + 1]].copy()
+        want[n_eff:] = 0
+        assert np.array_equal(H.unpack_np(got, n, n_eff, world, nw), want)
+        coded, dense = np.load(tmp_path / f"b{j}.npy")
+        assert coded < 0.5 * dense  # 60 % zero words: the coded exchange moves < half the bytes
+
+
 # ---------------------------------------------------------------------------------------------
 # GPU: emulated ranks in one process vs the standard solver
 # ---------------------------------------------------------------------------------------------
@@ -107,10 +185,59 @@ def test_hybrid_matches_solver_rmat(msbfs_pkg, world, K):
     qs = m.QuerySet.random(dg.n, K, 16, seed=K + world)
     with m.Solver(dg, "bitpar", max_groups=K) as s:
         ref = s.run(qs).F
-        got = H.emulate_ranks(s, qs, world)
+        got = H.emulate_ranks(s, qs, world)  # zero-word coded exchange (the default)
         assert np.array_equal(got, ref), (world, K)
+        if K in (1024, 5):
+            assert np.array_equal(H.emulate_ranks(s, qs, world, coded=False), ref), (world, K)
         # buffers are reused: the standard path still works after hybrid phases
         assert np.array_equal(s.run(qs).F, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,K", [(8, 1024), (3, 700), (2, 5)])
+def test_hybrid_coded_send_matches_numpy_codec(msbfs_pkg, world, K):
+    """k_code_bits/k_code_emit vs encode_np of the dense phase-A send segments, and the GPU
+    decode of every rank's received segments vs the dense exchange."""
+    import torch
+    m = msbfs_pkg
+    H = _H()
+    dg = m.DeviceGraph.rmat(14, 16, 5, device=0, relabel=True)
+    qs = m.QuerySet.random(dg.n, K, 16, seed=world)
+    n_eff = dg.hybrid_extent()
+    wbeg = H.word_split(K, world)
+    dev = torch.device("cuda", 0)
+    with m.Solver(dg, "bitpar", max_groups=K) as s:
+        dense_sends, coded_sends, lens = [], [], []
+        for r in range(world):
+            ss, _ = H.split_sizes(n_eff, wbeg, r)
+            bd = torch.empty(max(1, sum(ss)), dtype=torch.int64, device=dev)
+            s.hybrid_phase_a(qs, r, world, n_eff, r == 0, wbeg, bd.data_ptr())
+            bc = torch.empty(max(1, sum(H.coded_bound(x) for x in ss)), dtype=torch.int64,
+                             device=dev)
+            out, sa = s.hybrid_phase_a(qs, r, world, n_eff, r == 0, wbeg, bc.data_ptr(),
+                                       coded=True)
+            cl = [int(x) for x in sa["coded_len"]]
+            d = bd[:sum(ss)].cpu().numpy().view(np.uint64)
+            c = bc[:sum(cl)].cpu().numpy().view(np.uint64)
+            do, co = np.concatenate([[0], np.cumsum(ss)]), np.concatenate([[0], np.cumsum(cl)])
+            for j in range(world):
+                assert np.array_equal(c[co[j]:co[j + 1]], H.encode_np(d[do[j]:do[j + 1]])), (r, j)
+            dense_sends.append(d)
+            coded_sends.append(c)
+            lens.append(cl)
+        recvs = H.all_to_all_np(dense_sends, n_eff, wbeg)
+        for j in range(world):
+            nw = int(wbeg[j + 1] - wbeg[j])
+            if nw == 0:
+                continue
+            parts = [coded_sends[r][sum(lens[r][:j]):sum(lens[r][:j + 1])] for r in range(world)]
+            rc = torch.from_numpy(np.concatenate(parts).view(np.int64)).to(dev)
+            out = torch.full((max(1, len(recvs[j])),), -1, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            s.hybrid_decode(rc.data_ptr(), np.array([lens[r][j] for r in range(world)]), world,
+                            n_eff, nw, out.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(out[:len(recvs[j])].cpu().numpy().view(np.uint64), recvs[j]), j
 
 
 @pytest.mark.gpu

@@ -8,6 +8,7 @@ export PYTHONUNBUFFERED=1
 for spec in "$@"; do
   IFS='|' read -r name envs cmd <<< "$spec"
   echo "== $name: [$envs] $cmd"
+  [ "$envs" = "-" ] && envs=""
   env $envs timeout -k 10 "${EXP_LIMIT:-600}" $cmd > "gpurun_out/$name.log" 2>&1
   rc=$?
   echo "== $name rc=$rc"

@@ -133,6 +133,11 @@ for s in "$@"; do
           echo "$kv $(grep -o '"ms_per_step": [0-9.]*\|"level_ms": [^]]*' gpurun_out/k128_$n.log | tr '\n' ' ')"; done ;;
     pmclds) export TMPDIR=/tmp; rm -rf gpurun_out/pmcb3
          step pmcb3 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SMEM --kernel-include-regex "k_bu_chunks|k_bu_narrow" --output-format csv -d gpurun_out/pmcb3 -o run -- python bench.py --steps 1 --warmup 0 ;;
+    pmchbm) export TMPDIR=/tmp; R="k_bu|k_push|k_td|k_build|k_level"; rm -rf gpurun_out/pmch1 gpurun_out/pmch2 gpurun_out/pmch3
+         step pmch1 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmch1 -o run -- python bench.py --steps 1 --warmup 0 &&
+         step pmch2 300 rocprofv3 --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmch2 -o run -- python bench.py --steps 1 --warmup 0 &&
+         step pmch3 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT TA_BUSY_avr --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmch3 -o run -- python bench.py --steps 1 --warmup 0 &&
+         for d in pmch1 pmch2 pmch3; do python tools/prof_summary.py gpurun_out/$d > gpurun_out/$d.md; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -4,8 +4,8 @@
 Runs every rank's phase A (levels 1-2, own residue class of vertices) and phase C (own groups, levels >= 3)
 sequentially on one GPU (parallel/hybrid.py emulate_ranks), checks F against the single-GPU
 solver, and prints per-rank device times plus the all-to-all volume. The estimated N-GPU step
-is max_r(A_r) + exchange + max_r(C_r); the exchange is priced at --a2a-gbps per GPU (receive
-side), an assumption to be replaced by the driver's measured 8-GPU runs. For comparison it also
+is max_r(A_r) + exchange + max_r(C_r); the exchange (zero-word coded unless MSBFS_HYB_CODED=0) is priced at
+--a2a-gbps per GPU (max of send and receive side), an assumption to be replaced by the driver's measured 8-GPU runs. For comparison it also
 times round-robin (each rank runs ceil(K/N) groups on the whole graph).
 
     python tools/hybrid_sim.py --scale 26 --groups 1024 --ranks 2 4 8
@@ -62,6 +62,8 @@ def main():
             print(json.dumps({
                 "ranks": N, "correct": ok, "phase_a_ms_max": round(a, 3),
                 "phase_c_ms_max": round(c, 3), "a2a_MB_max": round(rb / 2**20, 1),
+                "a2a_dense_MB_max": round(max(x["dense_send_bytes"] for x in tim) / 2**20, 1),
+                "coded": H.coding_default(),
                 "a2a_ms_est": round(x_ms, 3), "hybrid_est_ms": round(a + x_ms + c, 3),
                 "roundrobin_ms_max": round(max(rr), 3),
                 "per_rank": [{k: (round(v, 3) if isinstance(v, float) else v)
