@@ -50,10 +50,12 @@ def main() -> int:
     ap.add_argument("--backend", default=None,
                     help="torch.distributed backend (default nccl = RCCL); gloo lets several ranks "
                          "share one GPU for testing")
-    ap.add_argument("--dist", default="auto", choices=["auto", "roundrobin", "hybrid"],
+    ap.add_argument("--dist", default="auto",
+                    choices=["auto", "roundrobin", "hybrid", "hybrid-coded"],
                     help="multi-GPU decomposition: round-robin query groups (main.cu:304-307) or "
-                         "hybrid (levels 1-2 vertex-partitioned, then query-partitioned); auto = "
-                         "run each feasible one once (untimed, max over ranks) and time the faster")
+                         "hybrid (levels 1-2 vertex-partitioned, then query-partitioned; its "
+                         "all-to-all dense or zero-word coded); auto = run each feasible one "
+                         "(untimed, max over ranks) and time the fastest")
     ap.add_argument("--relabel", type=int, default=1,
                     help="renumber vertices by descending degree after generation (preprocessing)")
     args = ap.parse_args()
@@ -86,15 +88,16 @@ def main() -> int:
                     and 1 <= qs.K <= solver.hybrid_max_groups())
     same_ids = D.allreduce_max(float(relabelled), ctx) == -D.allreduce_max(-float(relabelled), ctx)
     hybrid_ok = D.allreduce_max(0.0 if hybrid_local else 1.0, ctx) == 0.0 and same_ids
-    if args.dist == "hybrid" and not hybrid_ok:
+    if args.dist.startswith("hybrid") and not hybrid_ok:
         print("bench: hybrid mode needs >1 rank, --algo bitpar and K <= one pass", file=sys.stderr)
         return 2
-    candidates = {"auto": ["roundrobin", "hybrid"] if hybrid_ok else ["roundrobin"],
-                  "roundrobin": ["roundrobin"], "hybrid": ["hybrid"]}[args.dist]
+    candidates = {"auto": ["roundrobin", "hybrid", "hybrid-coded"] if hybrid_ok else ["roundrobin"],
+                  "roundrobin": ["roundrobin"], "hybrid": ["hybrid"],
+                  "hybrid-coded": ["hybrid-coded"]}[args.dist]
     plans = {}
     for m in candidates:
-        if m == "hybrid":
-            runner = H.HybridRunner(solver, qs.K, ctx)
+        if m.startswith("hybrid"):
+            runner = H.HybridRunner(solver, qs.K, ctx, coded=m == "hybrid-coded")
             plans[m] = (runner, runner.idx)
         else:
             rr = D.round_robin(qs.K, ctx.rank, ctx.world)
@@ -104,7 +107,7 @@ def main() -> int:
 
     def step(m):
         runner = plans[m][0]
-        if m == "hybrid":
+        if m.startswith("hybrid"):
             res = runner.run(qs)
             return res.F, res.stats
         r = solver.run(runner)  # round robin: the rank's query subset
@@ -180,7 +183,8 @@ def main() -> int:
                 "global_batch": qs.K,
                 "seq_len": args.group_size,
                 "parallelism": (f"hybrid{ctx.world} (levels 1-2 vertex-partitioned, then "
-                                f"query-partitioned)" if mode == "hybrid" else f"dp{ctx.world}"),
+                                f"query-partitioned{', coded exchange' if mode == 'hybrid-coded' else ''})"
+                                if mode.startswith("hybrid") else f"dp{ctx.world}"),
                 "algo": args.algo,
                 "n": g.n, "m": g.m,
                 "traversed_edges": total_edges,

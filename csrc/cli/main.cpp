@@ -328,9 +328,10 @@ int main(int argc, char* argv[]) {
     const int64_t nlocal = (int64_t)local_to_global.size();
     // hybrid exchange buffers: send = own range x all words (destination-major), recv = all
     // vertices x own words
-    // zero-word coded exchange (MSBFS_HYB_CODED=0: dense): send/receive coded segments, decode
-    // into hrecv; the phase-A SUM all-reduce also carries the P x P matrix of coded lengths
-    const bool hcoded = !(getenv("MSBFS_HYB_CODED") && atoi(getenv("MSBFS_HYB_CODED")) == 0);
+    // zero-word coded exchange (MSBFS_HYB_CODED=1; parallel/hybrid.py coding_default: it pays
+    // only below ~170 GB/s of all-to-all per GPU): send/receive coded segments, decode into
+    // hrecv; the phase-A SUM all-reduce also carries the P x P matrix of coded lengths
+    const bool hcoded = getenv("MSBFS_HYB_CODED") && atoi(getenv("MSBFS_HYB_CODED")) == 1;
     DevBuf hsend, hrecv, hrcoded;
     std::vector<int64_t> scount(P, 0), rcount(P, 0), hout, hF, clen(P, 0);
     const int nw_me = hybrid ? wbeg[me + 1] - wbeg[me] : 0;

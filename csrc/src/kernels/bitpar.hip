@@ -1905,6 +1905,34 @@ struct PartPrefix {
   int64_t b[kMaxParts + 1];  // b[r] = number of vertices owned by parts < r
 };
 
+// ---- zero-word coding of the hybrid exchange -------------------------------------------------
+// After level 2 about half of the exchanged 64-bit words are zero (RMAT-26, 1024 groups, 8
+// ranks: 50.5 %). A segment of L words (one destination's share) travels as ceil(L/64) bitmap
+// words (bit i of bitmap word c: word 64c+i is nonzero) followed by its nonzero words in order
+// (parallel/hybrid.py encode_np/decode_np are the reference twins). The sender packs the dense
+// segments (k_pack_words) and codes them 8 chunks of 64 words per wave (k_code_bits -> scan ->
+// k_code_emit: coalesced 512-byte chunk reads; coding straight from the visited rows read each
+// 128-byte row once per destination: 1.5 ms at 8 ranks); the receiver expands into the dense
+// layout phase C reads (k_decode_pop -> scan -> k_decode_emit). Chunks (64 words) are numbered
+// globally over the segments; a segment's chunks are [c0[j], c0[j+1]).
+// own vertices of part `part` of `nparts` below n_eff: v = part + i*nparts
+static inline int64_t part_count(int64_t n_eff, int part, int nparts) {
+  return n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
+}
+
+struct CodeSegs {
+  int64_t c0[kMaxParts + 1];  // first global chunk of each segment; c0[nseg] = total chunks
+  int64_t len[kMaxParts];     // dense words of each segment
+  int64_t base[kMaxParts];    // decode: coded start of each segment in the received buffer
+  int64_t dense[kMaxParts];   // decode: dense start of each segment
+};
+
+__device__ __forceinline__ int code_seg(const CodeSegs& cs, int nseg, int64_t c) {
+  int j = 0;
+  while (j + 1 < nseg && c >= cs.c0[j + 1]) ++j;
+  return j;
+}
+
 // send[cnt*wbeg[j] + i*nw_j + (w-wbeg[j])] = vis[v*W + w], v = part + i*nparts: destination-major
 // (rows of deg-0 vertices may be stale, see k_zero_src_rows: they are sent as zeros; phase C
 // never reads them either)
@@ -1926,85 +1954,82 @@ __global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, cons
   }
 }
 
-// ---- zero-word coding of the hybrid exchange -------------------------------------------------
-// After level 2 about half of the exchanged 64-bit words are zero (RMAT-26, 1024 groups, 8
-// ranks: 50.5 %). A segment of L words (one destination's share) travels as ceil(L/64) bitmap
-// words (bit i of bitmap word c: word 64c+i is nonzero) followed by its nonzero words in order
-// (parallel/hybrid.py encode_np/decode_np are the reference twins). The sender codes straight
-// from the visited rows (k_code_bits -> scan -> k_code_emit, reading the rows of nonzero words
-// twice instead of writing and re-reading a dense buffer); the receiver expands into the dense
-// layout phase C reads (k_decode_pop -> scan -> k_decode_emit). Chunks (64 words) are numbered
-// globally over the segments; a segment's chunks are [c0[j], c0[j+1]).
-// own vertices of part `part` of `nparts` below n_eff: v = part + i*nparts
-static inline int64_t part_count(int64_t n_eff, int part, int nparts) {
-  return n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
-}
+// Chunks per wave in the coding kernels: the loads of all of them are issued before any use
+// (one chunk per wave left the kernels bound by wave launches and single dependent loads).
+constexpr int kCodeCPW = 8;
 
-struct CodeSegs {
-  int64_t c0[kMaxParts + 1];  // first global chunk of each segment; c0[nseg] = total chunks
-  int64_t len[kMaxParts];     // dense words of each segment
-  int64_t base[kMaxParts];    // decode: coded start of each segment in the received buffer
-  int64_t dense[kMaxParts];   // decode: dense start of each segment
-};
-
-__device__ __forceinline__ int code_seg(const CodeSegs& cs, int nseg, int64_t c) {
-  int j = 0;
-  while (j + 1 < nseg && c >= cs.c0[j + 1]) ++j;
-  return j;
-}
-
-// word t of destination segment j in k_pack_words' order (0 for deg-0 vertices: stale rows)
-template <int W>
-__device__ __forceinline__ uint64_t code_word(const uint64_t* vis, const int64_t* rowptr, int part,
-                                              int nparts, const WordSplit& ws, int j, int64_t t) {
-  const int nw = ws.b[j + 1] - ws.b[j];
-  const int64_t i = t / nw;
-  const int64_t v = part + i * nparts;
-  if (rowptr[v + 1] == rowptr[v]) return 0ull;
-  return vis[v * W + ws.b[j] + (int)(t - i * nw)];
-}
-
-// one wave per chunk: bitmap word and its popcount
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_code_bits(const uint64_t* vis, const int64_t* rowptr,
-                                                      int part, int nparts, WordSplit ws,
-                                                      CodeSegs cs, int nseg, uint64_t* bits,
-                                                      int64_t* pop) {
+// bitmap word and popcount of every chunk of the dense segments in `dense` (segment j starts at
+// cs.dense[j])
+__global__ __launch_bounds__(kBlock) void k_code_bits(const uint64_t* dense, CodeSegs cs, int nseg,
+                                                      uint64_t* bits, int64_t* pop) {
   const int lane = lane_id();
   const int64_t nch = cs.c0[nseg];
-  for (int64_t c = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; c < nch;
-       c += ((int64_t)gridDim.x * kBlock) >> 6) {
-    const int j = code_seg(cs, nseg, c);
-    const int64_t t = (c - cs.c0[j]) * 64 + lane;
-    const uint64_t x = t < cs.len[j] ? code_word<W>(vis, rowptr, part, nparts, ws, j, t) : 0ull;
-    const uint64_t bm = __ballot(x != 0);
-    if (lane == 0) {
-      bits[c] = bm;
-      pop[c] = __popcll(bm);
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t cb = (((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * kCodeCPW; cb < nch;
+       cb += nwaves * kCodeCPW) {
+    uint64_t x[kCodeCPW];
+    int j = code_seg(cs, nseg, cb);
+#pragma unroll
+    for (int k = 0; k < kCodeCPW; ++k) {
+      const int64_t c = cb + k;
+      while (j + 1 < nseg && c >= cs.c0[j + 1]) ++j;
+      const int64_t t = (c - cs.c0[j]) * 64 + lane;
+      x[k] = (c < nch && t < cs.len[j]) ? dense[cs.dense[j] + t] : 0ull;
+    }
+    uint64_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < kCodeCPW; ++k) {
+      const uint64_t bm = __ballot(x[k] != 0);
+      if (lane == k) mine = bm;
+    }
+    if (lane < kCodeCPW && cb + lane < nch) {
+      bits[cb + lane] = mine;
+      pop[cb + lane] = __popcll(mine);
     }
   }
 }
 
 // incl = inclusive scan of pop. Segment j's coded start is c0[j] + X(c0[j]), X = exclusive
 // prefix: bitmap word of chunk c at c + X(c0[j]), its nonzero words from c0[j+1] + X(c).
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_code_emit(const uint64_t* vis, const int64_t* rowptr,
-                                                      int part, int nparts, WordSplit ws,
-                                                      CodeSegs cs, int nseg, const uint64_t* bits,
-                                                      const int64_t* incl, uint64_t* out) {
+__global__ __launch_bounds__(kBlock) void k_code_emit(const uint64_t* dense, CodeSegs cs, int nseg,
+                                                      const uint64_t* bits, const int64_t* incl,
+                                                      uint64_t* out) {
   const int lane = lane_id();
   const int64_t nch = cs.c0[nseg];
-  for (int64_t c = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; c < nch;
-       c += ((int64_t)gridDim.x * kBlock) >> 6) {
-    const int j = code_seg(cs, nseg, c);
-    const uint64_t bm = bits[c];
-    const int64_t x = incl[c] - __popcll(bm);
-    const int64_t cj = cs.c0[j];
-    if (lane == 0) out[c + incl[cj] - __popcll(bits[cj])] = bm;
-    if ((bm >> lane) & 1ull) {
-      const int64_t t = (c - cj) * 64 + lane;
-      out[cs.c0[j + 1] + x + __popcll(bm & lanemask_lt())] =
-          code_word<W>(vis, rowptr, part, nparts, ws, j, t);
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t cb = (((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * kCodeCPW; cb < nch;
+       cb += nwaves * kCodeCPW) {
+    // lane k < CPW holds chunk cb+k's bitmap, inclusive prefix and segment start offset
+    uint64_t bml = 0;
+    int64_t incl_l = 0, xj_l = 0;
+    int jl = 0;
+    if (lane < kCodeCPW && cb + lane < nch) {
+      const int64_t c = cb + lane;
+      jl = code_seg(cs, nseg, c);
+      bml = bits[c];
+      incl_l = incl[c];
+      const int64_t cj = cs.c0[jl];
+      xj_l = incl[cj] - __popcll(bits[cj]);
+    }
+    uint64_t x[kCodeCPW];
+#pragma unroll
+    for (int k = 0; k < kCodeCPW; ++k) {  // every data load first
+      const uint64_t bm = __shfl(bml, k);
+      const int j = __shfl(jl, k);
+      const int64_t c = cb + k;
+      x[k] = (c < nch && ((bm >> lane) & 1ull))
+                 ? dense[cs.dense[j] + (c - cs.c0[j]) * 64 + lane] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kCodeCPW; ++k) {
+      const int64_t c = cb + k;
+      if (c >= nch) break;
+      const uint64_t bm = __shfl(bml, k);
+      const int j = __shfl(jl, k);
+      const int64_t xc = __shfl(incl_l, k) - __popcll(bm);
+      const int64_t xj = __shfl(xj_l, k);
+      if (lane == 0) out[c + xj] = bm;
+      if ((bm >> lane) & 1ull) out[cs.c0[j + 1] + xc + __popcll(bm & lanemask_lt())] = x[k];
     }
   }
 }
@@ -2029,25 +2054,43 @@ __global__ __launch_bounds__(kBlock) void k_decode_pop(const uint64_t* in, CodeS
   }
 }
 
-// one wave per received chunk: its 64 dense words (zeros included)
+// kCodeCPW received chunks per wave: their 64 dense words each (zeros included)
 __global__ __launch_bounds__(kBlock) void k_decode_emit(const uint64_t* in, CodeSegs cs, int nseg,
                                                         const int64_t* incl, uint64_t* dense) {
   const int lane = lane_id();
   const int64_t nch = cs.c0[nseg];
-  for (int64_t d = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; d < nch;
-       d += ((int64_t)gridDim.x * kBlock) >> 6) {
-    const int r = code_seg(cs, nseg, d);
-    const int64_t d0 = cs.c0[r], q = d - d0;
-    const uint64_t* seg = in + cs.base[r];
-    const uint64_t bm = seg[q];
-    // nonzero words before this chunk in segment r
-    const int64_t before = (incl[d] - __popcll(bm)) - (incl[d0] - __popcll(seg[0]));
-    const int64_t t = q * 64 + lane;
-    if (t < cs.len[r]) {
-      uint64_t x = 0;
-      if ((bm >> lane) & 1ull)
-        x = seg[(cs.c0[r + 1] - d0) + before + __popcll(bm & lanemask_lt())];
-      dense[cs.dense[r] + t] = x;
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t db = (((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * kCodeCPW; db < nch;
+       db += nwaves * kCodeCPW) {
+    // lane k < CPW: chunk db+k's segment, bitmap word and data start
+    uint64_t bml = 0;
+    int64_t data_l = 0;
+    int rl = 0;
+    if (lane < kCodeCPW && db + lane < nch) {
+      const int64_t d = db + lane;
+      rl = code_seg(cs, nseg, d);
+      const int64_t d0 = cs.c0[rl];
+      const uint64_t* seg = in + cs.base[rl];
+      bml = seg[d - d0];
+      // nonzero words before this chunk in segment r
+      const int64_t before = (incl[d] - __popcll(bml)) - (incl[d0] - __popcll(seg[0]));
+      data_l = cs.base[rl] + (cs.c0[rl + 1] - d0) + before;
+    }
+    uint64_t x[kCodeCPW];
+#pragma unroll
+    for (int k = 0; k < kCodeCPW; ++k) {
+      const uint64_t bm = __shfl(bml, k);
+      const int64_t dl = __shfl(data_l, k);  // every lane takes part in the shuffle
+      x[k] = (db + k < nch && ((bm >> lane) & 1ull)) ? in[dl + __popcll(bm & lanemask_lt())]
+                                                     : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kCodeCPW; ++k) {
+      const int64_t d = db + k;
+      if (d >= nch) break;
+      const int r = __shfl(rl, k);
+      const int64_t t = (d - cs.c0[r]) * 64 + lane;
+      if (t < cs.len[r]) dense[cs.dense[r] + t] = x[k];
     }
   }
 }
@@ -2092,7 +2135,8 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
     V<VW> x = vzero<VW>();
     int64_t deg = 0;
     if (v < n_eff) {
-      const uint64_t* src = recv + (pre.b[v % nparts] + v / nparts) * nw;
+      const uint32_t vq = (uint32_t)v / (uint32_t)nparts;  // ids < 2^31: 32-bit division
+      const uint64_t* src = recv + (pre.b[(uint32_t)v - vq * (uint32_t)nparts] + vq) * nw;
       if (slot == 0) deg = rowptr[v + 1] - rowptr[v];
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
@@ -2440,13 +2484,15 @@ class BitparSolver final : public Solver {
     int64_t* incl;
     void* tmp;
     size_t tmp_bytes;
+    uint64_t* dense;  // sender: the dense segments (dense_words)
   };
-  CodeWs code_ws(int64_t chunks) {
+  CodeWs code_ws(int64_t chunks, int64_t dense_words = 0) {
     const size_t a = ((size_t)chunks * 8 + 255) & ~size_t(255);
-    const size_t tb = inclusive_scan_temp_bytes(chunks);
-    code_ws_.ensure(3 * a + tb);
+    const size_t tb = (inclusive_scan_temp_bytes(chunks) + 255) & ~size_t(255);
+    code_ws_.ensure(3 * a + tb + (size_t)dense_words * 8);
     char* p = (char*)code_ws_.p;
-    return CodeWs{(uint64_t*)p, (int64_t*)(p + a), (int64_t*)(p + 2 * a), p + 3 * a, tb};
+    return CodeWs{(uint64_t*)p, (int64_t*)(p + a), (int64_t*)(p + 2 * a), p + 3 * a, tb,
+                  (uint64_t*)(p + 3 * a + tb)};
   }
 
   // zero-word coded send segments of phase A (see k_code_bits); coded_len[j] (host) = words of
@@ -2455,22 +2501,26 @@ class BitparSolver final : public Solver {
   void code_send(const uint64_t* vis, int64_t cnt, int part, int nparts, const WordSplit& ws,
                  uint64_t* send, int64_t* coded_len, hipStream_t s) {
     CodeSegs cs{};
-    int64_t c = 0;
+    int64_t c = 0, dn = 0;
     for (int j = 0; j < nparts; ++j) {
       cs.c0[j] = c;
       cs.len[j] = cnt * (ws.b[j + 1] - ws.b[j]);
+      cs.dense[j] = dn;
       c += (cs.len[j] + 63) / 64;
+      dn += cs.len[j];
     }
     cs.c0[nparts] = c;
     for (int j = 0; j < nparts; ++j) coded_len[j] = 0;
     if (c == 0) return;
-    const CodeWs w = code_ws(c);
-    k_code_bits<W><<<grid_for(c * 64, kBlock, 8192), kBlock, 0, s>>>(
-        vis, g_.rowptr, part, nparts, ws, cs, nparts, w.bits, w.pop);
+    const CodeWs w = code_ws(c, dn);
+    k_pack_words<W><<<grid_for(cnt * ws.b[nparts], kBlock, 8192), kBlock, 0, s>>>(
+        vis, g_.rowptr, part, nparts, cnt, ws.b[nparts], ws, w.dense);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    const int gc = grid_for((c + kCodeCPW - 1) / kCodeCPW * 64, kBlock, 1 << 20);
+    k_code_bits<<<gc, kBlock, 0, s>>>(w.dense, cs, nparts, w.bits, w.pop);
     MSBFS_HIP_CHECK(hipGetLastError());
     inclusive_scan_i64(w.pop, w.incl, c, w.tmp, w.tmp_bytes, s);
-    k_code_emit<W><<<grid_for(c * 64, kBlock, 8192), kBlock, 0, s>>>(
-        vis, g_.rowptr, part, nparts, ws, cs, nparts, w.bits, w.incl, send);
+    k_code_emit<<<gc, kBlock, 0, s>>>(w.dense, cs, nparts, w.bits, w.incl, send);
     MSBFS_HIP_CHECK(hipGetLastError());
     k_code_lens<<<1, 64, 0, s>>>(cs, nparts, w.bits, w.incl, w.pop);  // pop is free again
     MSBFS_HIP_CHECK(hipGetLastError());
@@ -2502,11 +2552,11 @@ class BitparSolver final : public Solver {
     cs.c0[nparts] = c;
     if (c == 0) return;
     const CodeWs w = code_ws(c);
-    k_decode_pop<<<grid_for(c, kBlock, 8192), kBlock, 0, s>>>(coded, cs, nparts, w.pop);
+    k_decode_pop<<<grid_for(c, kBlock, 1 << 20), kBlock, 0, s>>>(coded, cs, nparts, w.pop);
     MSBFS_HIP_CHECK(hipGetLastError());
     inclusive_scan_i64(w.pop, w.incl, c, w.tmp, w.tmp_bytes, s);
-    k_decode_emit<<<grid_for(c * 64, kBlock, 8192), kBlock, 0, s>>>(coded, cs, nparts, w.incl,
-                                                                     dense);
+    k_decode_emit<<<grid_for((c + kCodeCPW - 1) / kCodeCPW * 64, kBlock, 1 << 20), kBlock, 0,
+                    s>>>(coded, cs, nparts, w.incl, dense);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
 

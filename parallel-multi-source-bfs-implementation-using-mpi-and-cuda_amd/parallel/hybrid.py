@@ -15,10 +15,11 @@ keeps the replica but changes the split:
            isolated vertices in the suffix, which is never sent), the words of its own group
            block (1/N of the words); plus one small SUM all-reduce of the phase-A partial sums,
            "still alive" flags and frontier sizes. About half of those words are zero after
-           level 2 (RMAT-26, 1024 groups, 8 ranks: 50.5 %), so each destination's share travels
+           level 2 (RMAT-26, 1024 groups, 8 ranks: 50.5 %): optionally (coded=True, bench
+           candidate "hybrid-coded", MSBFS_HYB_CODED=1) each destination's share travels
            zero-word coded (encode_np: a bitmap word per 64 words + the nonzero words; the
            same all-reduce carries the N x N matrix of coded lengths) and the receiver expands
-           it on the GPU (Solver.hybrid_decode).
+           it on the GPU (Solver.hybrid_decode); see coding_default for when that pays.
   phase C  every rank continues its own groups from level 3 (bit-parallel, as in round-robin).
 
 Result: F[k] = reduced[k] + F_C[k] for the own groups; the global argmin is the usual 8-byte
@@ -30,6 +31,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 import os
+import time
 from typing import Optional
 
 import numpy as np
@@ -75,8 +77,11 @@ def coded_bound(words: int) -> int:
 
 
 def coding_default() -> bool:
-    """Zero-word coded exchange unless MSBFS_HYB_CODED=0 (A/B knob)."""
-    return os.environ.get("MSBFS_HYB_CODED", "1") != "0"
+    """Zero-word coded exchange only with MSBFS_HYB_CODED=1. Measured (RMAT-26, 1024 groups, 8
+    ranks emulated on one MI355X): 296 instead of 501 MB per GPU, but +0.8 ms of coding in phase
+    A and +0.43 ms of decoding before phase C, so it pays only when the all-to-all runs below
+    ~170 GB/s per GPU. bench.py measures it as a separate candidate ("hybrid-coded")."""
+    return os.environ.get("MSBFS_HYB_CODED", "0") == "1"
 
 
 def encode_np(words: np.ndarray) -> np.ndarray:
@@ -303,8 +308,12 @@ def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
             dense = torch.empty(max(1, sum(split_sizes(n_eff, wbeg, j)[1])), dtype=torch.int64,
                                 device=dev)
             torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
             solver.hybrid_decode(rt.data_ptr(), np.array(rsz, np.int64), world, n_eff, nw,
                                  dense.data_ptr())
+            torch.cuda.synchronize(dev)
+            if timings is not None:  # wall time of the GPU decode (launches + kernels)
+                timings[len(timings) - world + j]["decode_ms"] = (time.perf_counter() - t0) * 1e3
             rt = dense
         Fc, sc = solver.hybrid_phase_c(K, int(wbeg[j]), nw, world, n_eff, rt.data_ptr(), reduced)
         if timings is not None:

@@ -21,7 +21,7 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("dist", ["hybrid", "roundrobin", "auto"])
+@pytest.mark.parametrize("dist", ["hybrid", "hybrid-coded", "roundrobin", "auto"])
 def test_bench_forced_rccl_one_rank(dist):
     env = dict(os.environ, MSBFS_FORCE_DIST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
                RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
@@ -32,10 +32,11 @@ def test_bench_forced_rccl_one_rank(dist):
     assert r.returncode == 0, r.stderr[-3000:]
     js = json.loads(r.stdout.strip().splitlines()[-1])
     assert js["n_gpus"] == 1 and js["value"] > 0
-    if dist == "hybrid":
+    if dist.startswith("hybrid"):
         assert js["config"]["parallelism"].startswith("hybrid1")
+        assert ("coded" in js["config"]["parallelism"]) == (dist == "hybrid-coded")
     if dist == "auto":
-        assert set(js["config"]["candidates_ms"]) == {"roundrobin", "hybrid"}
+        assert set(js["config"]["candidates_ms"]) == {"roundrobin", "hybrid", "hybrid-coded"}
 
 
 def test_bench_graph_forced_rccl_one_rank(msbfs_pkg):
@@ -75,7 +76,7 @@ def test_bench_graph_two_ranks_gloo(msbfs_pkg):
     assert js["traversed_edges"] == int(ref.edges.sum())
 
 
-@pytest.mark.parametrize("ranks,dist", [(2, "hybrid"), (3, "auto")])
+@pytest.mark.parametrize("ranks,dist", [(2, "hybrid"), (2, "hybrid-coded"), (3, "auto")])
 def test_bench_multi_rank_gloo_shared_gpu(ranks, dist):
     """bench.py with several ranks on the one GPU (gloo collectives, the hybrid exchange staged
     through host memory): every rank runs its own solver, the hybrid phases exchange real
@@ -89,7 +90,7 @@ def test_bench_multi_rank_gloo_shared_gpu(ranks, dist):
     assert r.returncode == 0, r.stderr[-3000:]
     js = json.loads(r.stdout.strip().splitlines()[-1])
     assert js["n_gpus"] == ranks and js["value"] > 0
-    if dist == "hybrid":
+    if dist.startswith("hybrid"):
         assert js["config"]["parallelism"].startswith(f"hybrid{ranks}")
     else:
-        assert set(js["config"]["candidates_ms"]) == {"roundrobin", "hybrid"}
+        assert set(js["config"]["candidates_ms"]) == {"roundrobin", "hybrid", "hybrid-coded"}

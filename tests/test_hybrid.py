@@ -185,10 +185,10 @@ def test_hybrid_matches_solver_rmat(msbfs_pkg, world, K):
     qs = m.QuerySet.random(dg.n, K, 16, seed=K + world)
     with m.Solver(dg, "bitpar", max_groups=K) as s:
         ref = s.run(qs).F
-        got = H.emulate_ranks(s, qs, world)  # zero-word coded exchange (the default)
+        got = H.emulate_ranks(s, qs, world)  # dense exchange (the default)
         assert np.array_equal(got, ref), (world, K)
-        if K in (1024, 5):
-            assert np.array_equal(H.emulate_ranks(s, qs, world, coded=False), ref), (world, K)
+        # zero-word coded exchange, decoded on the GPU
+        assert np.array_equal(H.emulate_ranks(s, qs, world, coded=True), ref), (world, K)
         # buffers are reused: the standard path still works after hybrid phases
         assert np.array_equal(s.run(qs).F, ref)
 
@@ -289,3 +289,5 @@ def test_hybrid_runner_single_process(msbfs_pkg):
         res = H.hybrid_bfs(s, qs)
         assert np.array_equal(res.idx, np.arange(qs.K))
         assert np.array_equal(res.F, ref)
+        coded = H.HybridRunner(s, qs.K, H.D.DistContext(device=0), coded=True).run(qs)
+        assert np.array_equal(coded.F, ref) and coded.stats["coded"]

@@ -4,7 +4,7 @@
 Runs every rank's phase A (levels 1-2, own residue class of vertices) and phase C (own groups, levels >= 3)
 sequentially on one GPU (parallel/hybrid.py emulate_ranks), checks F against the single-GPU
 solver, and prints per-rank device times plus the all-to-all volume. The estimated N-GPU step
-is max_r(A_r) + exchange + max_r(C_r); the exchange (zero-word coded unless MSBFS_HYB_CODED=0) is priced at
+is max_r(A_r) + exchange + max_r(C_r); the exchange (dense; zero-word coded with MSBFS_HYB_CODED=1) is priced at
 --a2a-gbps per GPU (max of send and receive side), an assumption to be replaced by the driver's measured 8-GPU runs. For comparison it also
 times round-robin (each rank runs ceil(K/N) groups on the whole graph).
 
@@ -52,7 +52,7 @@ def main():
             F = H.emulate_ranks(s, qs, N, timings=tim)
             ok = bool(np.array_equal(F, ref.F))
             a = max(x["phase_a_ms"] for x in tim)
-            c = max(x["phase_c_ms"] for x in tim)
+            c = max(x["phase_c_ms"] + x.get("decode_ms", 0.0) for x in tim)  # decode: receiver
             rb = max(max(x["recv_bytes"], x["send_bytes"]) for x in tim)
             x_ms = rb / (args.a2a_gbps * 1e9) * 1e3
             rr = [0.0]
