@@ -2135,8 +2135,7 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
     V<VW> x = vzero<VW>();
     int64_t deg = 0;
     if (v < n_eff) {
-      const uint32_t vq = (uint32_t)v / (uint32_t)nparts;  // ids < 2^31: 32-bit division
-      const uint64_t* src = recv + (pre.b[(uint32_t)v - vq * (uint32_t)nparts] + vq) * nw;
+      const uint64_t* src = recv + (pre.b[v % nparts] + v / nparts) * nw;
       if (slot == 0) deg = rowptr[v + 1] - rowptr[v];
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
@@ -2266,6 +2265,7 @@ class BitparSolver final : public Solver {
     if (const char* x = getenv("MSBFS_NARROW_C")) narrow_c_ = atoi(x);
     if (const char* x = getenv("MSBFS_COOP")) coop_ = atoi(x);
     if (const char* x = getenv("MSBFS_GAMMA")) gamma_ = atof(x);
+    if (const char* x = getenv("MSBFS_GAMMA2")) gamma2_ = atof(x);
     if (const char* x = getenv("MSBFS_LAZY")) lazy_ = atoi(x);
     if (const char* x = getenv("MSBFS_TD_FUSED")) td_fused_ = atoi(x);
     if (const char* x = getenv("MSBFS_TD_BM")) td_bm_min_ = atoll(x);
@@ -2653,6 +2653,7 @@ class BitparSolver final : public Solver {
   double alpha_low_ = 4.0;
   DevBuf asnap_;        // any-visited bitmap at the start of a lazy batch's first pull level
   double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
+  double gamma2_ = -1;  // MSBFS_GAMMA2: the same test for level 2 (< 0: gamma_)
   int coop_ = -1;      // MSBFS_COOP: cross-chunk early exit on the first pull level (-1 auto)
   int narrow_c_ = 2;   // MSBFS_NARROW_C: short first narrow step (0 off, 1 always, 2 by level)
   int hub_big_ = 3;  // MSBFS_HUBBIG: bit 0 narrow, bit 1 chunks use a 128-KB LDS hub bitmap
@@ -2779,7 +2780,9 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       // (RMAT-30, 256 groups: 742 -> 294 ms/step; RMAT-26, 16 groups: 16.4 -> 9.3 ms; road
       // graphs never get there). MSBFS_GAMMA scales the vertex test (0 turns it off).
       bottom_up = (double)S.ef > (double)S.ea / alpha_eff() ||
-                  (gamma_ > 0 && S.level >= 1 && (double)S.ef > gamma_ * (double)n_eff());
+                  (gamma_ > 0 && S.level >= 1 &&
+                   (double)S.ef > (S.level == 1 && gamma2_ >= 0 ? gamma2_ : gamma_) *
+                                      (double)n_eff());
     else bottom_up = !((double)S.nf < (double)S.na / opt.beta && (double)S.ef < (double)S.ea / alpha_eff());
     if (S.level < dirs_.size() && (dirs_[S.level] == 'T' || dirs_[S.level] == 'B'))
       bottom_up = dirs_[S.level] == 'B';
