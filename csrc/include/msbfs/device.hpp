@@ -183,11 +183,12 @@ int64_t hybrid_extent(const DeviceGraph& g);
 
 std::unique_ptr<Solver> make_bitpar_solver(const DeviceGraph& g, int max_groups);
 
-// MSBFS_ALGO_AUTO for `groups` groups per solver pass: the per-group distance BFS for up to 3
-// groups (RMAT-26: 3.2 ms per group; a bit-parallel pass of 1-4 groups takes 10-16 ms, its
-// per-vertex work does not shrink with the group count), bit-parallel otherwise and on
-// low-degree graphs (road grid 4896^2, one group: 70 ms bit-parallel vs 114 ms distance BFS).
-constexpr int64_t kAutoDistMaxGroups = 3;
+// MSBFS_ALGO_AUTO for `groups` groups per solver pass: the per-group distance BFS for up to 2
+// groups (RMAT-26: 3.7 / 7.1 ms for 1 / 2 groups vs 10.1 / 12.4 ms bit-parallel, whose
+// per-vertex work does not shrink with the group count; 3 groups: 9.5 vs 8.4 ms), bit-parallel
+// otherwise and on low-degree graphs (road grid 4896^2, one group: 70 ms bit-parallel vs 114 ms
+// distance BFS).
+constexpr int64_t kAutoDistMaxGroups = 2;
 inline int auto_device_algo(const DeviceGraph& g, int64_t groups) {
   return (groups <= kAutoDistMaxGroups && g.max_degree > 64) ? 2 /* dist */ : 1 /* bitpar */;
 }

@@ -2653,7 +2653,10 @@ class BitparSolver final : public Solver {
   double alpha_low_ = 4.0;
   DevBuf asnap_;        // any-visited bitmap at the start of a lazy batch's first pull level
   double gamma_ = 1.0;  // MSBFS_GAMMA: push -> pull once frontier edges > gamma * n_eff
-  double gamma2_ = -1;  // MSBFS_GAMMA2: the same test for level 2 (< 0: gamma_)
+  // MSBFS_GAMMA2: the same test for level 2 (< 0: gamma_). Lower, because only level 2 can pull
+  // with prefix pull + tail push: a push level 2 makes level 3 the first pull, which scans whole
+  // rows (RMAT-30, 16 groups: level 3 277 ms; 296 -> 106 ms/step; RMAT-26, 4 groups 15.5 -> 8.7)
+  double gamma2_ = 0.25;
   int coop_ = -1;      // MSBFS_COOP: cross-chunk early exit on the first pull level (-1 auto)
   int narrow_c_ = 2;   // MSBFS_NARROW_C: short first narrow step (0 off, 1 always, 2 by level)
   int hub_big_ = 3;  // MSBFS_HUBBIG: bit 0 narrow, bit 1 chunks use a 128-KB LDS hub bitmap
