@@ -1905,6 +1905,11 @@ struct PartPrefix {
   int64_t b[kMaxParts + 1];  // b[r] = number of vertices owned by parts < r
 };
 
+// own vertices of part `part` of `nparts` below n_eff: v = part + i*nparts
+static inline int64_t part_count(int64_t n_eff, int part, int nparts) {
+  return n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
+}
+
 // ---- zero-word coding of the hybrid exchange -------------------------------------------------
 // After level 2 about half of the exchanged 64-bit words are zero (RMAT-26, 1024 groups, 8
 // ranks: 50.5 %). A segment of L words (one destination's share) travels as ceil(L/64) bitmap
@@ -1915,11 +1920,6 @@ struct PartPrefix {
 // 128-byte row once per destination: 1.5 ms at 8 ranks); the receiver expands into the dense
 // layout phase C reads (k_decode_pop -> scan -> k_decode_emit). Chunks (64 words) are numbered
 // globally over the segments; a segment's chunks are [c0[j], c0[j+1]).
-// own vertices of part `part` of `nparts` below n_eff: v = part + i*nparts
-static inline int64_t part_count(int64_t n_eff, int part, int nparts) {
-  return n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
-}
-
 struct CodeSegs {
   int64_t c0[kMaxParts + 1];  // first global chunk of each segment; c0[nseg] = total chunks
   int64_t len[kMaxParts];     // dense words of each segment
