@@ -1,3 +1,6 @@
+#!/bin/bash
+# A/B of the level-2 push -> pull threshold (MSBFS_GAMMA2) over few-group RMAT-26/30, RMAT-22 and
+# uniform graphs (round 2: chose gamma2 = 0.25). Run on the GPU box: bash tools/gamma_exp.sh
 set -u
 mkdir -p gpurun_out
 run() { # name env args...

@@ -1,3 +1,6 @@
+#!/bin/bash
+# Follow-up to gamma_exp.sh with the new default: bit-parallel vs distance BFS for 1-3 groups
+# (sets kAutoDistMaxGroups) and the headline / RMAT-30 configs for regressions.
 set -u
 mkdir -p gpurun_out
 run() { # name env args...
