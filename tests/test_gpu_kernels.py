@@ -395,3 +395,25 @@ def test_bitpar_fused_level_records_match(msbfs_pkg, monkeypatch):
                 recs[fused] = [(r["level"], r["dir"], r["nf"], r["ef"], r["nf_next"])
                                for r in s.level_trace()]
         assert recs["1"] == recs["0"], K
+
+
+@pytest.mark.parametrize("gamma2,want", [("0", "B"), ("100", "T")])
+def test_bitpar_level2_direction_threshold(msbfs_pkg, monkeypatch, gamma2, want):
+    """MSBFS_GAMMA2 decides level 2's direction for few groups: a pull with the prefix pull + tail
+    push (0) or a push that makes level 3 the first, whole-row pull (100). Both plans must give
+    the oracle's F; the level records show which one ran."""
+    m = msbfs_pkg
+    monkeypatch.setenv("MSBFS_GAMMA2", gamma2)
+    monkeypatch.setenv("MSBFS_GAMMA", "100")  # the later levels' vertex test out of the way
+    dg = m.DeviceGraph.rmat(16, 16, 9, device=0)
+    hg = dg.download()
+    dg.relabel_by_degree()
+    for K in (4, 32):
+        qs = m.QuerySet.random(hg.n, K, 16, seed=K)
+        ref = m.cpu_bfs(hg, qs)
+        # a tiny alpha turns Beamer's edge test off: only the vertex test decides
+        with m.Solver(dg, "bitpar", max_groups=K, alpha=1e-9) as s:
+            r = s.run(qs)
+            dirs = "".join(t["dir"] for t in s.level_trace())
+        assert np.array_equal(r.F, ref.F), (gamma2, K, dirs)
+        assert dirs[:2] == "T" + want, (gamma2, K, dirs)
