@@ -3,10 +3,12 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <mutex>
 
 #include "msbfs/device.hpp"
 
@@ -47,6 +49,17 @@ void Comm::alltoallv_device_u64(const uint64_t* send, const std::vector<int64_t>
   MSBFS_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+void Comm::allreduce_min_u64_async(uint64_t x, int slot) {
+  if (slot < 0 || slot >= kAsyncSlots) fail("async all-reduce slot out of range");
+  if ((int)async_vals_.size() <= slot) async_vals_.resize(slot + 1, ~0ull);
+  async_vals_[slot] = allreduce_min_u64(x);
+}
+
+void Comm::wait_async(uint64_t* results, int nslots) {
+  for (int i = 0; i < nslots; ++i) results[i] = i < (int)async_vals_.size() ? async_vals_[i] : ~0ull;
+  async_vals_.clear();
+}
+
 namespace {
 
 class LocalComm final : public Comm {
@@ -71,6 +84,148 @@ class LocalComm final : public Comm {
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
   }
   [[noreturn]] void abort(int code) override { std::exit(code); }
+};
+
+}  // namespace
+
+// ---- ThreadComm: ranks = threads of one process ------------------------------------------------
+struct ThreadGroup {
+  explicit ThreadGroup(int n) : size(n), ptrs(n), cptrs(n), vals(n), dvals(n), counts(n) {}
+  const int size;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  // per-rank slots published between two barriers
+  std::vector<void*> ptrs;
+  std::vector<const void*> cptrs;
+  std::vector<uint64_t> vals;
+  std::vector<double> dvals;
+  std::vector<const std::vector<int64_t>*> counts;
+  void sync() {
+    std::unique_lock<std::mutex> l(m);
+    const uint64_t g = gen;
+    if (++arrived == size) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(l, [&] { return gen != g; });
+    }
+  }
+};
+
+namespace {
+
+class ThreadComm final : public Comm {
+ public:
+  ThreadComm(std::shared_ptr<ThreadGroup> g, int rank) : g_(std::move(g)), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int size() const override { return g_->size; }
+  std::string name() const override { return "threads"; }
+  void barrier() override { g_->sync(); }
+  void bcast_host(void* p, size_t bytes, int root) override {
+    if (rank_ == root) g_->cptrs[root] = p;
+    g_->sync();
+    if (rank_ != root && bytes) std::memcpy(p, g_->cptrs[root], bytes);
+    g_->sync();  // the root's buffer stays valid until every copy is done
+  }
+  void bcast_device(void* dptr, size_t bytes, int root, hipStream_t s) override {
+    if (rank_ == root) g_->cptrs[root] = dptr;
+    int dev = 0;
+    MSBFS_HIP_CHECK(hipGetDevice(&dev));
+    g_->vals[rank_] = (uint64_t)dev;
+    g_->sync();
+    if (rank_ != root && bytes) {
+      MSBFS_HIP_CHECK(hipMemcpyPeerAsync(dptr, dev, g_->cptrs[root], (int)g_->vals[root], bytes, s));
+      MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    g_->sync();
+  }
+  uint64_t allreduce_min_u64(uint64_t x) override {
+    g_->vals[rank_] = x;
+    g_->sync();
+    uint64_t r = x;
+    for (uint64_t v : g_->vals) r = std::min(r, v);
+    g_->sync();
+    return r;
+  }
+  void allreduce_sum_i64(int64_t* p, size_t n) override {
+    g_->cptrs[rank_] = p;
+    g_->sync();
+    std::vector<int64_t> t(n, 0);
+    for (int r = 0; r < g_->size; ++r) {
+      const int64_t* q = (const int64_t*)g_->cptrs[r];
+      for (size_t i = 0; i < n; ++i) t[i] += q[i];
+    }
+    g_->sync();  // everyone has read every input before anyone overwrites its own
+    if (n) std::memcpy(p, t.data(), n * 8);
+  }
+  double allreduce_max_f64(double x) override {
+    g_->dvals[rank_] = x;
+    g_->sync();
+    double r = x;
+    for (double v : g_->dvals) r = std::max(r, v);
+    g_->sync();
+    return r;
+  }
+  void allgather_u64(uint64_t x, std::vector<uint64_t>& out) override {
+    g_->vals[rank_] = x;
+    g_->sync();
+    out = g_->vals;
+    g_->sync();
+  }
+  // offset of rank r's block for rank `me` inside r's send buffer
+  int64_t send_offset(int r, int me) const {
+    int64_t o = 0;
+    for (int k = 0; k < me; ++k) o += (*g_->counts[r])[k];
+    return o;
+  }
+  void alltoallv_host_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                          uint64_t* recv, const std::vector<int64_t>& rcount) override {
+    g_->cptrs[rank_] = send;
+    g_->counts[rank_] = &scount;
+    g_->sync();
+    int64_t ro = 0;
+    for (int r = 0; r < g_->size; ++r) {
+      if (rcount[r] != (*g_->counts[r])[rank_]) fail("threads all-to-all: count mismatch");
+      std::memcpy(recv + ro, (const uint64_t*)g_->cptrs[r] + send_offset(r, rank_), rcount[r] * 8);
+      ro += rcount[r];
+    }
+    g_->sync();
+  }
+  void alltoallv_device_u64(const uint64_t* send, const std::vector<int64_t>& scount,
+                            uint64_t* recv, const std::vector<int64_t>& rcount,
+                            hipStream_t s) override {
+    int dev = 0;
+    MSBFS_HIP_CHECK(hipGetDevice(&dev));
+    g_->cptrs[rank_] = send;
+    g_->counts[rank_] = &scount;
+    g_->vals[rank_] = (uint64_t)dev;
+    g_->sync();
+    // every receiver pulls its pieces (peer copies over xGMI when the ranks own different GPUs)
+    int64_t ro = 0;
+    for (int r = 0; r < g_->size; ++r) {
+      if (rcount[r] != (*g_->counts[r])[rank_]) fail("threads all-to-all: count mismatch");
+      if (rcount[r])
+        MSBFS_HIP_CHECK(hipMemcpyPeerAsync(recv + ro, dev,
+                                           (const uint64_t*)g_->cptrs[r] + send_offset(r, rank_),
+                                           (int)g_->vals[r], rcount[r] * 8, s));
+      ro += rcount[r];
+    }
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    g_->sync();
+  }
+  [[noreturn]] void abort(int code) override {
+    // one process is the whole job: end it (peer threads may be blocked in a collective)
+    fflush(stdout);
+    fflush(stderr);
+    std::_Exit(code);
+  }
+
+ private:
+  std::shared_ptr<ThreadGroup> g_;
+  int rank_;
 };
 
 #ifdef MSBFS_HAVE_MPI
@@ -136,6 +291,22 @@ class MpiComm : public Comm {
     }
     if (!req.empty()) MPI_Waitall((int)req.size(), req.data(), MPI_STATUSES_IGNORE);
   }
+  void allreduce_min_u64_async(uint64_t x, int slot) override {
+    if (slot < 0 || slot >= kAsyncSlots) fail("async all-reduce slot out of range");
+    if (in_.empty()) {  // fixed storage: buffers of in-flight requests never move
+      in_.assign(kAsyncSlots, ~0ull);
+      out_.assign(kAsyncSlots, ~0ull);
+      req_.assign(kAsyncSlots, MPI_REQUEST_NULL);
+    }
+    in_[slot] = x;
+    nused_ = std::max(nused_, slot + 1);
+    MPI_Iallreduce(&in_[slot], &out_[slot], 1, MPI_UINT64_T, MPI_MIN, MPI_COMM_WORLD, &req_[slot]);
+  }
+  void wait_async(uint64_t* results, int nslots) override {
+    if (nused_) MPI_Waitall(nused_, req_.data(), MPI_STATUSES_IGNORE);
+    for (int i = 0; i < nslots; ++i) results[i] = i < nused_ ? out_[i] : ~0ull;
+    nused_ = 0;
+  }
   [[noreturn]] void abort(int code) override {
     // unlike main.cu:98,140 (exit without MPI_Abort -> peers hang in MPI_Bcast), take the job down
     MPI_Abort(MPI_COMM_WORLD, code);
@@ -144,41 +315,58 @@ class MpiComm : public Comm {
 
  private:
   int rank_ = 0, size_ = 1;
+  // in-flight asynchronous all-reduces (kAsyncSlots entries allocated once)
+  std::vector<uint64_t> in_, out_;
+  std::vector<MPI_Request> req_;
+  int nused_ = 0;
 };
 #endif
 
-#if defined(MSBFS_HAVE_MPI) && defined(MSBFS_HAVE_RCCL)
+#ifdef MSBFS_HAVE_RCCL
 #define NCCL_CHECK(x)                                                                     \
   do {                                                                                    \
     ncclResult_t r_ = (x);                                                                \
     if (r_ != ncclSuccess) ::msbfs::fail(std::string("RCCL error: ") + ncclGetErrorString(r_)); \
   } while (0)
 
+// RCCL prints a version banner on stdout at init; the report on stdout must stay the
+// reference's 7 lines (main.cu:403-414), so the banner goes to stderr
+template <class F>
+ncclResult_t quiet_init(F&& f) {
+  fflush(stdout);
+  const int saved = dup(1);
+  if (saved >= 0) dup2(2, 1);
+  const ncclResult_t r = f();
+  fflush(stdout);
+  if (saved >= 0) {
+    dup2(saved, 1);
+    close(saved);
+  }
+  return r;
+}
+
 class RcclComm final : public Comm {
  public:
+  // one process per GPU: unique id over the host communicator, ncclCommInitRank
   RcclComm(std::unique_ptr<Comm> host, int device) : host_(std::move(host)), device_(device) {
     ncclUniqueId id;
     if (host_->rank() == 0) NCCL_CHECK(ncclGetUniqueId(&id));
     host_->bcast_host(&id, sizeof(id), 0);
     MSBFS_HIP_CHECK(hipSetDevice(device_));
-    MSBFS_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    // RCCL prints a version banner on stdout at init; the report on stdout must stay the
-    // reference's 7 lines (main.cu:403-414), so the banner goes to stderr
-    fflush(stdout);
-    const int saved = dup(1);
-    if (saved >= 0) dup2(2, 1);
-    const ncclResult_t r = ncclCommInitRank(&comm_, host_->size(), id, host_->rank());
-    fflush(stdout);
-    if (saved >= 0) {
-      dup2(saved, 1);
-      close(saved);
-    }
-    NCCL_CHECK(r);
-    MSBFS_HIP_CHECK(hipMalloc(&scratch_, 64));
+    NCCL_CHECK(quiet_init([&] { return ncclCommInitRank(&comm_, host_->size(), id, host_->rank()); }));
+    setup();
+  }
+  // single-process mode: a communicator made by ncclCommInitAll for this rank's device
+  RcclComm(std::unique_ptr<Comm> host, int device, ncclComm_t comm)
+      : host_(std::move(host)), device_(device), comm_(comm) {
+    MSBFS_HIP_CHECK(hipSetDevice(device_));
+    setup();
   }
   ~RcclComm() override {
     if (comm_) ncclCommDestroy(comm_);
     if (scratch_) (void)hipFree(scratch_);
+    if (hstage_) (void)hipHostFree(hstage_);
+    if (hkeys_) (void)hipHostFree(hkeys_);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
   int rank() const override { return host_->rank(); }
@@ -196,22 +384,41 @@ class RcclComm final : public Comm {
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
   }
   uint64_t allreduce_min_u64(uint64_t x) override {
-    MSBFS_HIP_CHECK(hipMemcpyAsync(scratch_, &x, 8, hipMemcpyHostToDevice, stream_));
-    NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclUint64, ncclMin, comm_, stream_));
-    uint64_t r;
-    MSBFS_HIP_CHECK(hipMemcpyAsync(&r, scratch_, 8, hipMemcpyDeviceToHost, stream_));
+    uint64_t* hk = hkeys_ + 2 * kAsyncSlots;  // a slot of its own (not an async slot)
+    hk[0] = x;
+    MSBFS_HIP_CHECK(hipMemcpyAsync(key_dev(kAsyncSlots), hk, 8, hipMemcpyHostToDevice, stream_));
+    NCCL_CHECK(ncclAllReduce(key_dev(kAsyncSlots), key_dev(kAsyncSlots), 1, ncclUint64, ncclMin,
+                             comm_, stream_));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(hk + 1, key_dev(kAsyncSlots), 8, hipMemcpyDeviceToHost, stream_));
     MSBFS_HIP_CHECK(hipStreamSynchronize(stream_));
-    return r;
+    return hk[1];
   }
+  void reserve_device_scratch(size_t bytes) override { ensure(bytes); }
   void allreduce_sum_i64(int64_t* p, size_t n) override {
     if (!n) return;
-    void* d = nullptr;
-    MSBFS_HIP_CHECK(hipMalloc(&d, n * 8));
-    MSBFS_HIP_CHECK(hipMemcpyAsync(d, p, n * 8, hipMemcpyHostToDevice, stream_));
+    ensure(n * 8);  // persistent: reserve_device_scratch() sizes it before any timed region
+    std::memcpy(hstage_, p, n * 8);
+    int64_t* d = (int64_t*)((char*)scratch_ + kKeyBytes);
+    MSBFS_HIP_CHECK(hipMemcpyAsync(d, hstage_, n * 8, hipMemcpyHostToDevice, stream_));
     NCCL_CHECK(ncclAllReduce(d, d, n, ncclInt64, ncclSum, comm_, stream_));
-    MSBFS_HIP_CHECK(hipMemcpyAsync(p, d, n * 8, hipMemcpyDeviceToHost, stream_));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(hstage_, d, n * 8, hipMemcpyDeviceToHost, stream_));
     MSBFS_HIP_CHECK(hipStreamSynchronize(stream_));
-    (void)hipFree(d);
+    std::memcpy(p, hstage_, n * 8);
+  }
+  // issued on the communicator's stream: runs beside the caller's next kernels
+  void allreduce_min_u64_async(uint64_t x, int slot) override {
+    if (slot < 0 || slot >= kAsyncSlots) fail("async all-reduce slot out of range");
+    hkeys_[slot] = x;
+    MSBFS_HIP_CHECK(hipMemcpyAsync(key_dev(slot), hkeys_ + slot, 8, hipMemcpyHostToDevice, stream_));
+    NCCL_CHECK(ncclAllReduce(key_dev(slot), key_dev(slot), 1, ncclUint64, ncclMin, comm_, stream_));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(hkeys_ + kAsyncSlots + slot, key_dev(slot), 8,
+                                   hipMemcpyDeviceToHost, stream_));
+    nasync_ = std::max(nasync_, slot + 1);
+  }
+  void wait_async(uint64_t* results, int nslots) override {
+    MSBFS_HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int i = 0; i < nslots; ++i) results[i] = i < nasync_ ? hkeys_[kAsyncSlots + i] : ~0ull;
+    nasync_ = 0;
   }
   double allreduce_max_f64(double x) override { return host_->allreduce_max_f64(x); }
   void allgather_u64(uint64_t x, std::vector<uint64_t>& out) override {
@@ -244,11 +451,32 @@ class RcclComm final : public Comm {
   }
 
  private:
+  // device scratch: (kAsyncSlots + 1) key slots, then the all-reduce staging area
+  static constexpr size_t kKeyBytes = ((size_t)(kAsyncSlots + 1) * 8 + 255) & ~size_t(255);
+  uint64_t* key_dev(int slot) const { return (uint64_t*)scratch_ + slot; }
+  void setup() {
+    MSBFS_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    MSBFS_HIP_CHECK(hipHostMalloc((void**)&hkeys_, (2 * kAsyncSlots + 2) * 8, hipHostMallocDefault));
+    ensure(64 << 10);
+  }
+  void ensure(size_t bytes) {
+    if (bytes <= cap_ && scratch_) return;
+    const size_t cap = std::max(bytes, cap_ * 2);
+    if (scratch_) (void)hipFree(scratch_);
+    if (hstage_) (void)hipHostFree(hstage_);
+    MSBFS_HIP_CHECK(hipMalloc(&scratch_, kKeyBytes + cap));
+    MSBFS_HIP_CHECK(hipHostMalloc(&hstage_, cap, hipHostMallocDefault));
+    cap_ = cap;
+  }
   std::unique_ptr<Comm> host_;
   int device_;
   ncclComm_t comm_ = nullptr;
-  hipStream_t stream_ = nullptr;
+  hipStream_t stream_ = nullptr;  // the communicator's own stream (collectives, async keys)
   void* scratch_ = nullptr;
+  void* hstage_ = nullptr;        // pinned staging of allreduce_sum_i64
+  uint64_t* hkeys_ = nullptr;     // pinned: async inputs, async results, one sync slot pair
+  size_t cap_ = 0;
+  int nasync_ = 0;
 };
 #endif
 
@@ -275,7 +503,7 @@ std::unique_ptr<Comm> maybe_upgrade_rccl(std::unique_ptr<Comm> host, const std::
   // still runs every device collective: the RCCL code paths on a one-GPU box)
   if (want == "mpi" || want == "local" || device < 0 || (host->size() == 1 && want != "rccl"))
     return host;
-#if defined(MSBFS_HAVE_MPI) && defined(MSBFS_HAVE_RCCL)
+#ifdef MSBFS_HAVE_RCCL
   // RCCL needs one rank per GPU: check (host, device) pairs are unique across the job.
   char hn[256] = {0};
   gethostname(hn, sizeof(hn) - 1);
@@ -293,6 +521,33 @@ std::unique_ptr<Comm> maybe_upgrade_rccl(std::unique_ptr<Comm> host, const std::
 #else
   if (want == "rccl" && host->rank() == 0)
     fprintf(stderr, "msbfs: built without RCCL/MPI; using %s\n", host->name().c_str());
+  return host;
+#endif
+}
+
+std::vector<std::unique_ptr<Comm>> make_thread_comms(int nranks) {
+  auto g = std::make_shared<ThreadGroup>(nranks);
+  std::vector<std::unique_ptr<Comm>> out;
+  for (int r = 0; r < nranks; ++r) out.push_back(std::make_unique<ThreadComm>(g, r));
+  return out;
+}
+
+std::vector<std::unique_ptr<Comm>> upgrade_thread_comms_rccl(
+    std::vector<std::unique_ptr<Comm>> host, const std::vector<int>& devices) {
+#ifdef MSBFS_HAVE_RCCL
+  const int n = (int)host.size();
+  std::vector<int> d(devices);
+  std::sort(d.begin(), d.end());
+  if (n < 1 || (int)devices.size() != n || std::adjacent_find(d.begin(), d.end()) != d.end())
+    return host;  // RCCL needs one rank per GPU
+  std::vector<ncclComm_t> comms(n);
+  NCCL_CHECK(quiet_init([&] { return ncclCommInitAll(comms.data(), n, devices.data()); }));
+  std::vector<std::unique_ptr<Comm>> out;
+  for (int r = 0; r < n; ++r)
+    out.push_back(std::make_unique<RcclComm>(std::move(host[r]), devices[r], comms[r]));
+  return out;
+#else
+  (void)devices;
   return host;
 #endif
 }

@@ -9,10 +9,12 @@
 //   --algo {auto,bitpar,dist,topdown,sweep,cpu}   --comm {auto,mpi,rccl,local}
 //   --gen rmat:SCALE:EF:SEED | uniform:N:M:SEED   (per-rank device generation, no broadcast)
 //   --qgen K:SIZE:SEED                            (generated query groups)
+//   --tune key=value,...   bit-parallel solver tuning (see msbfs_solver_tune in msbfs.h)
 //   --threads N (cpu algo)  --cache (CSR sidecar, off by default like the reference's re-read;
 //   --no-cache is accepted)  --json  --sort-rows  --no-relabel  --repeat R
-//   --dist {auto,roundrobin,hybrid}  multi-rank decomposition (auto: hybrid when > 1 rank, the
-//          bit-parallel solver and K <= one pass; see kernels/bitpar.hip "hybrid")
+//   --dist {auto,roundrobin,hybrid,hybrid-coded}  multi-rank decomposition (auto: hybrid when > 1
+//          rank, the bit-parallel solver and K <= one pass; see kernels/bitpar "hybrid";
+//          hybrid-coded: the same with the zero-word coded all-to-all)
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -35,7 +37,7 @@ using clk = std::chrono::high_resolution_clock;
 namespace {
 
 struct Args {
-  std::string graph, query, algo = "auto", comm = "auto", gen, qgen, dist = "auto";
+  std::string graph, query, algo = "auto", comm = "auto", gen, qgen, dist = "auto", tune;
   int numGPU = 1;
   int threads = 0;
   int repeat = 1;
@@ -103,6 +105,7 @@ int main(int argc, char* argv[]) {
     else if (!strcmp(argv[i], "--dist") && has) a.dist = argv[++i];
     else if (!strcmp(argv[i], "--gen") && has) a.gen = argv[++i];
     else if (!strcmp(argv[i], "--qgen") && has) a.qgen = argv[++i];
+    else if (!strcmp(argv[i], "--tune") && has) a.tune = argv[++i];
     else if (!strcmp(argv[i], "--threads") && has) a.threads = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--repeat") && has) a.repeat = std::max(1, atoi(argv[++i]));
     else if (!strcmp(argv[i], "--cache")) a.cache = true;
@@ -263,8 +266,15 @@ int main(int argc, char* argv[]) {
     }
     const int64_t K = q.K();
 
-    if (a.dist != "auto" && a.dist != "roundrobin" && a.dist != "hybrid")
+    if (a.dist != "auto" && a.dist != "roundrobin" && a.dist != "hybrid" &&
+        a.dist != "hybrid-coded")
       fail("unknown --dist " + a.dist);
+    // zero-word coded exchange (parallel/hybrid.py coding_default: it pays only below ~170 GB/s
+    // of all-to-all per GPU): send/receive coded segments, decode into hrecv; the phase-A SUM
+    // all-reduce also carries the P x P matrix of coded lengths. A command-line choice, agreed
+    // below with the hybrid eligibility (every rank must size and call the same collectives).
+    const bool want_coded = a.dist == "hybrid-coded";
+    if (want_coded) a.dist = "hybrid";
     const int P = comm->size(), me = comm->rank();
     int dalgo = algo;
     if (!cpu && dalgo == 0)
@@ -284,6 +294,7 @@ int main(int argc, char* argv[]) {
         if (dalgo == 3) solver->opt.force_dir = 1;
       }
       if (a.json) solver->opt.count_edges = true;
+      if (!a.tune.empty()) solver->tune(a.tune);
       MSBFS_HIP_CHECK(hipDeviceSynchronize());
     }
     // Every rank must take the same branch (the two modes call different collectives), but
@@ -294,7 +305,10 @@ int main(int argc, char* argv[]) {
     // (the hybrid exchange moves rows by vertex id: every rank must number vertices alike)
     const bool same_ids = comm->allreduce_min_u64(relabelled ? 1 : 0) == 1 ||
                           comm->allreduce_min_u64(relabelled ? 0 : 1) == 1;
-    const bool hybrid = comm->allreduce_min_u64(hybrid_local ? 1 : 0) == 1 && same_ids;
+    // one MIN all-reduce: bit 1 = hybrid-eligible here, bit 0 = coded exchange requested here
+    const uint64_t agree = comm->allreduce_min_u64((hybrid_local ? 2u : 0u) | (want_coded ? 1u : 0u));
+    const bool hybrid = agree >= 2 && same_ids;
+    const bool hcoded = hybrid && (agree & 1u);
     if (a.dist == "hybrid" && !hybrid && me == 0)
       fprintf(stderr,
               "msbfs: --dist hybrid needs --algo bitpar, <= %d ranks and K <= one pass on every "
@@ -328,10 +342,6 @@ int main(int argc, char* argv[]) {
     const int64_t nlocal = (int64_t)local_to_global.size();
     // hybrid exchange buffers: send = own range x all words (destination-major), recv = all
     // vertices x own words
-    // zero-word coded exchange (MSBFS_HYB_CODED=1; parallel/hybrid.py coding_default: it pays
-    // only below ~170 GB/s of all-to-all per GPU): send/receive coded segments, decode into
-    // hrecv; the phase-A SUM all-reduce also carries the P x P matrix of coded lengths
-    const bool hcoded = getenv("MSBFS_HYB_CODED") && atoi(getenv("MSBFS_HYB_CODED")) == 1;
     DevBuf hsend, hrecv, hrcoded;
     std::vector<int64_t> scount(P, 0), rcount(P, 0), hout, hF, clen(P, 0);
     const int nw_me = hybrid ? wbeg[me + 1] - wbeg[me] : 0;

@@ -130,12 +130,17 @@ class Solver {
   // of reached vertices, i.e. 2x the Graph500 traversed-edge count) are written to host memory.
   virtual void run(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t* F,
                    int64_t* edges2, RunStats* st, hipStream_t stream) = 0;
+  // Algorithm tuning, "key=value,key=value" (bit-parallel solver: see bp::Tuning in
+  // kernels/bitpar/solver.hpp). Unknown keys are errors; solvers without tuning reject any.
+  virtual void tune(const std::string& spec) {
+    if (!spec.empty()) fail("this solver has no tuning keys (got '" + spec + "')");
+  }
 
   // ---- hybrid multi-GPU mode (bit-parallel solver only) ------------------------------------
   // Levels 1-2 run vertex-partitioned (every rank: all K groups, pulls only for its residue
   // class of vertices v = part + i*nparts < n_eff); one all-to-all hands every rank its own
   // words (groups) for all vertices; the remaining levels run query-partitioned. See
-  // kernels/bitpar.hip "hybrid". Largest K one hybrid round supports (0: not supported).
+  // kernels/bitpar/hybrid.hpp. Largest K one hybrid round supports (0: not supported).
   virtual int64_t hybrid_max_groups() const { return 0; }
   // Largest number of ranks (vertex parts) one hybrid round supports.
   static constexpr int kHybridMaxParts = 64;

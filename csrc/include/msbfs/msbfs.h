@@ -19,7 +19,7 @@ typedef struct msbfs_graph_s* msbfs_graph;
 typedef struct msbfs_solver_s* msbfs_solver;
 
 enum msbfs_algo {
-  MSBFS_ALGO_AUTO = 0,    /* dist for <= 3 groups on graphs with max degree > 64, else bit-parallel */
+  MSBFS_ALGO_AUTO = 0,    /* dist for <= 2 groups on graphs with max degree > 64, else bit-parallel */
   MSBFS_ALGO_BITPAR = 1,  /* 64*W groups per pass, direction optimising */
   MSBFS_ALGO_DIST = 2,    /* one distance array per group, direction optimising */
   MSBFS_ALGO_TOPDOWN = 3, /* dist path, top-down only (queue + load-balanced edges) */
@@ -105,6 +105,11 @@ void msbfs_graph_free(msbfs_graph g);
 /* ---- solvers ---- */
 int msbfs_solver_create(msbfs_graph g, int algo, int64_t max_groups, msbfs_solver* out);
 int msbfs_solver_set_options(msbfs_solver s, const msbfs_options* o);
+/* Algorithm tuning "key=value,key=value" (bit-parallel solver keys: gamma gamma2 pfx codes
+ * code_deg lean lean_min lazy td_fused td_bm batch dirs; defaults are the measured best).
+ * Unknown keys or bad values fail with an error; other solvers accept only an empty spec. The
+ * process-wide defaults come from MSBFS_TUNE (same syntax, read once, echoed on stderr). */
+int msbfs_solver_tune(msbfs_solver s, const char* spec);
 /* F[k] for k in [0,K); edges2 (nullable) = per-group sum of reached degrees (2x the Graph500
  * traversed-edge count). stream = hipStream_t or NULL for the null stream. */
 int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32_t* qids,

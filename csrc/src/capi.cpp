@@ -377,6 +377,13 @@ int msbfs_solver_set_options(msbfs_solver s, const msbfs_options* o) {
   });
 }
 
+int msbfs_solver_tune(msbfs_solver s, const char* spec) {
+  return guard([&] {
+    if (!spec) msbfs::fail("msbfs_solver_tune: null spec");
+    s->impl->tune(spec);
+  });
+}
+
 int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32_t* qids,
                      int64_t* F, int64_t* edges2, msbfs_stats* st, void* stream) {
   return guard([&] {

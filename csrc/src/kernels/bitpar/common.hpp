@@ -1,0 +1,349 @@
+// Bit-parallel MS-BFS: row layout, wave helpers, level counters and the per-level reductions
+// shared by every translation unit of the solver (kernels/bitpar_*.hip). Design overview:
+// solver.hpp.
+#pragma once
+
+#include <cstdint>
+
+#include "msbfs/device.hpp"
+#include "msbfs/device_lists.hpp"
+
+namespace msbfs {
+namespace bp {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kChunk = 1024;      // bottom-up edge chunk for wide vertices
+constexpr int kMaxGrid = 2048;    // blocks of the grid-stride level kernels
+constexpr int kSmallDeg = 64;     // max degree for the vertex-parallel top-down expansion
+
+template <int W>
+struct Lay {
+  static constexpr int VW = W >= 2 ? 2 : 1;
+  static constexpr int G = W / VW;      // lanes per vertex
+  static constexpr int VPW = 64 / G;    // vertices per wave
+  static constexpr int TILE = kWaves * VPW;  // vertices per block iteration
+  static constexpr uint64_t GBITS = (G == 64) ? ~0ull : ((1ull << G) - 1);
+};
+
+template <int VW>
+struct V {
+  uint64_t w[VW];
+};
+
+template <int VW>
+__device__ __forceinline__ V<VW> ldv(const uint64_t* p) {
+  V<VW> r;
+  if constexpr (VW == 2) {
+    typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+    const u2 x = *(const u2*)p;
+    r.w[0] = x.x;
+    r.w[1] = x.y;
+  } else {
+    r.w[0] = *p;
+  }
+  return r;
+}
+template <int VW>
+__device__ __forceinline__ void stv(uint64_t* p, const V<VW>& v) {
+  if constexpr (VW == 2) {
+    typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+    u2 x;
+    x.x = v.w[0];
+    x.y = v.w[1];
+    *(u2*)p = x;
+  } else {
+    *p = v.w[0];
+  }
+}
+template <int VW>
+__device__ __forceinline__ V<VW> vzero() {
+  V<VW> r;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) r.w[j] = 0;
+  return r;
+}
+
+// Wave-uniform copies (SGPRs) of values every lane holds identically: keeps loops over them
+// uniform (scalar branches) instead of exec-masked "divergent" loops.
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int32_t uni32(int32_t x) {
+  return (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
+struct Ctr {
+  Slot32 act2, actw2, fl2, touched;
+  Slot64 ef2;  // sum of degrees of the next frontier
+  Slot64 eu2;  // sum of degrees of the next active lists
+  Slot64 ev2;  // sum of degrees of vertices visited for the first time (by any group)
+};
+// host view of the interesting fields
+struct HostCtr {
+  uint32_t act2, actw2, fl2, touched;
+  unsigned long long ef2, eu2, ev2;
+};
+
+__device__ __forceinline__ bool is_done(const uint32_t* done, int32_t v) {
+  return (done[v >> 5] >> (v & 31)) & 1u;
+}
+__device__ __forceinline__ void set_done(uint32_t* done, int32_t v) {
+  atomicOr(&done[v >> 5], 1u << (v & 31));
+}
+// anyvis: bit v set once vertex v is visited by any group. A clear bit guarantees both visited
+// buffers of v are all-zero (bits are set before/with the first non-zero store and never
+// cleared within a batch), so pulls may skip the 8*W-byte load; a set bit only costs a load.
+__device__ __forceinline__ bool any_visited(const uint32_t* anyvis, int32_t u) {
+  return (anyvis[u >> 5] >> (u & 31)) & 1u;
+}
+
+// ---- per-group level counters in LDS ------------------------------------------------------------
+template <int W, bool COUNT>
+struct Lds {
+  uint32_t f[64 * W];
+  unsigned long long e[COUNT ? 64 * W : 1];
+};
+
+template <int W, bool COUNT>
+__device__ __forceinline__ void lds_zero(Lds<W, COUNT>& s) {
+  for (int i = threadIdx.x; i < 64 * W; i += blockDim.x) {
+    s.f[i] = 0;
+    if constexpr (COUNT) s.e[i] = 0;
+  }
+}
+
+template <int W, bool COUNT>
+__device__ __forceinline__ void count_bits(Lds<W, COUNT>& s, const V<Lay<W>::VW>& nw, int slot,
+                                           uint32_t deg) {
+  constexpr int VW = Lay<W>::VW;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    uint64_t x = nw.w[j];
+    const int base = (slot * VW + j) * 64;
+    while (x) {
+      const int b = __ffsll((unsigned long long)x) - 1;
+      x &= x - 1;
+      atomicAdd(&s.f[base + b], 1u);
+      if constexpr (COUNT) atomicAdd(&s.e[base + b], (unsigned long long)deg);
+    }
+  }
+}
+
+// Per-block counter row -> slab row blockIdx.x (plain stores; no same-address atomics). The
+// level's rows are summed by k_level_reduce.
+template <int W, bool COUNT>
+__device__ __forceinline__ void slab_store(Lds<W, COUNT>& s, uint32_t* slabF,
+                                           unsigned long long* slabE) {
+  __syncthreads();
+  uint32_t* rf = slabF + (size_t)blockIdx.x * (64 * W);
+  for (int i = threadIdx.x; i < 64 * W; i += blockDim.x) {
+    rf[i] = s.f[i];
+    if constexpr (COUNT) slabE[(size_t)blockIdx.x * (64 * W) + i] = s.e[i];
+  }
+}
+
+// Register-resident bit-sliced (carry-save) counters: bit b of c[j][d] is bit d of the count of
+// group (slot*VW + j)*64 + b. Adding a 64-bit new-bits word costs 2*D branch-free ops, vs one
+// LDS atomic per set bit in a divergent loop. Spilled to LDS every < 2^D additions.
+template <int VW, int DD = 6>
+struct BitCounter {
+  static constexpr int D = DD;
+  uint64_t c[VW][D];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int j = 0; j < VW; ++j)
+#pragma unroll
+      for (int d = 0; d < D; ++d) c[j][d] = 0;
+  }
+  __device__ __forceinline__ void add(const V<VW>& x) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      uint64_t carry = x.w[j];
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const uint64_t t = c[j][d] & carry;
+        c[j][d] ^= carry;
+        carry = t;
+      }
+    }
+  }
+  template <int W, bool COUNT>
+  __device__ __forceinline__ void spill(Lds<W, COUNT>& s, int slot) {
+    spill(s.f, slot);
+  }
+  __device__ __forceinline__ void spill(uint32_t* f, int slot) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      uint64_t any = 0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) any |= c[j][d];
+      const int base = (slot * VW + j) * 64;
+      while (any) {
+        const int b = __ffsll((unsigned long long)any) - 1;
+        any &= any - 1;
+        uint32_t v = 0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) v |= (uint32_t)((c[j][d] >> b) & 1ull) << d;
+        atomicAdd(&f[base + b], v);
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) c[j][d] = 0;
+    }
+  }
+  // Same, into rows of STRIDE words per 64 groups. STRIDE = 65 skews the groups of different
+  // lane slots onto different LDS banks: with 64 every lane of the wave hit the bank of bit b
+  // (level-3 k_bu_narrow counted ~5e8 bank-conflict cycles; RMAT-26 levels 3 / 4 6.46 / 2.53 ->
+  // 6.22 / 2.46 ms with 65). Summing the sub-groups' counts with shuffles before one atomic per
+  // slot measured slower (a 64-step wave-uniform bit loop: 27.2 ms/step).
+  template <int STRIDE>
+  __device__ __forceinline__ void spill_strided(uint32_t* f, int slot) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      uint64_t any = 0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) any |= c[j][d];
+      const int base = (slot * VW + j) * STRIDE;
+      while (any) {
+        const int b = __ffsll((unsigned long long)any) - 1;
+        any &= any - 1;
+        uint32_t v = 0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) v |= (uint32_t)((c[j][d] >> b) & 1ull) << d;
+        atomicAdd(&f[base + b], v);
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) c[j][d] = 0;
+    }
+  }
+};
+
+// Sum the level's slab rows: block (word, row-group); lane = group bit. F += level * count
+// (`level` is the weight: 0 for a level another rank of the hybrid mode accounts for),
+// alive_next |= groups with count > 0 (one ballot + one atomicOr per word per row-group).
+template <int W, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
+                                                         const unsigned long long* slabE, int rows,
+                                                         int rgroups, unsigned long long* F,
+                                                         unsigned long long* E,
+                                                         uint64_t* alive_next, uint32_t level) {
+  __shared__ unsigned long long pf[kWaves][64], pe[kWaves][64];
+  const int word = blockIdx.x % W, rg = blockIdx.x / W;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  const int r0 = (int)((int64_t)rows * rg / rgroups);
+  const int r1 = (int)((int64_t)rows * (rg + 1) / rgroups);
+  const int i = word * 64 + lane;
+  unsigned long long f = 0, e = 0;
+  for (int r = r0 + wv; r < r1; r += kWaves) {
+    f += slabF[(size_t)r * (64 * W) + i];
+    if constexpr (COUNT) e += slabE[(size_t)r * (64 * W) + i];
+  }
+  pf[wv][lane] = f;
+  pe[wv][lane] = e;
+  __syncthreads();
+  if (wv == 0) {
+    for (int w = 1; w < kWaves; ++w) {
+      f += pf[w][lane];
+      e += pe[w][lane];
+    }
+    if (f) atomicAdd(&F[i], f * level);
+    if constexpr (COUNT) {
+      if (e) atomicAdd(&E[i], e);
+    }
+    const uint64_t m = __ballot(f != 0);
+    if (lane == 0 && m) atomicOr((unsigned long long*)&alive_next[word], m);
+  }
+}
+
+// k_level_reduce over the slab rows of nlev consecutive levels (`rows` rows each, level j's rows
+// first-level-major) of the device-driven batches: F += sum_j weight(level_first + j) * count_j;
+// alive_next + 16 * j = the groups with new vertices at level j (the mask after it). One launch
+// per few levels (a launch costs ~5 us, a road-like graph's level 15-200 us); the levels in
+// between read an older alive mask, a superset, which only lets them mark fewer vertices done.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_level_reduce_multi(const uint32_t* slabF, int rows,
+                                                               int nlev, int rgroups,
+                                                               uint32_t level_first, int weight_l1,
+                                                               unsigned long long* F,
+                                                               uint64_t* alive_next) {
+  __shared__ uint32_t pl[kWaves][64];
+  const int word = blockIdx.x % W, rg = blockIdx.x / W;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  const int r0 = (int)((int64_t)rows * rg / rgroups);
+  const int r1 = (int)((int64_t)rows * (rg + 1) / rgroups);
+  const int i = word * 64 + lane;
+  unsigned long long fw = 0;
+  for (int j = 0; j < nlev; ++j) {
+    uint32_t f = 0;
+    for (int r = r0 + wv; r < r1; r += kWaves) f += slabF[((size_t)j * rows + r) * (64 * W) + i];
+    pl[wv][lane] = f;
+    __syncthreads();
+    if (wv == 0) {
+      for (int w = 1; w < kWaves; ++w) f += pl[w][lane];
+      const uint32_t lvl = level_first + (uint32_t)j;
+      fw += (unsigned long long)f * ((lvl == 1 && !weight_l1) ? 0u : lvl);
+      const uint64_t m = __ballot(f != 0);
+      if (lane == 0 && m) atomicOr((unsigned long long*)&alive_next[16 * j + word], m);
+    }
+    __syncthreads();
+  }
+  if (wv == 0 && fw) atomicAdd(&F[i], fw);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-level accounting, once per level over the NEW frontier list (kept out of the traversal
+// kernels so they keep their occupancy): new bits of v = visNew[v] & ~visOld[v] after a
+// bottom-up level (DIFF) or acc[v] after a top-down level. G lanes per vertex; counts go to
+// register bit-sliced counters (or, for the edge-count mode, per-bit LDS atomics weighted by
+// degree), then to this block's slab row.
+// ---------------------------------------------------------------------------------------------
+template <int W, bool COUNT, bool DIFF>
+__global__ __launch_bounds__(kBlock) void k_count_frontier(const int32_t* fl, const Ctr* ctr,
+                                                           const int64_t* rowptr,
+                                                           const uint64_t* a,
+                                                           const uint64_t* b, uint32_t* slabF,
+                                                           unsigned long long* slabE) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  __shared__ Lds<W, COUNT> s;
+  lds_zero(s);
+  __syncthreads();
+  const int64_t nf = ctr->fl2.v;
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nf; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t idx = tb + wv * VPW + sub;
+    V<VW> nw = vzero<VW>();
+    uint32_t deg = 0;
+    if (idx < nf) {
+      const int32_t v = fl[idx];
+      const int64_t vo = (int64_t)v * W + slot * VW;
+      nw = ldv<VW>(a + vo);
+      if constexpr (DIFF) {
+        const V<VW> o = ldv<VW>(b + vo);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) nw.w[j] &= ~o.w[j];
+      }
+      if constexpr (COUNT) deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
+    }
+    if constexpr (COUNT) {
+      count_bits<W, COUNT>(s, nw, slot, deg);
+    } else {
+      bc.add(nw);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.spill(s, slot);
+        nadd = 0;
+      }
+    }
+  }
+  if constexpr (!COUNT) bc.spill(s, slot);
+  slab_store<W, COUNT>(s, slabF, slabE);
+}
+
+}  // namespace bp
+}  // namespace msbfs

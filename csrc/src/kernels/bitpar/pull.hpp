@@ -1,0 +1,926 @@
+// Bit-parallel MS-BFS: bottom-up (pull) level kernels — active lists, sparse row codes, prefix
+// pull + tail push, the narrow lane-group pull, the lean first-row pass, hub edge chunks and the
+// wide finalize.
+#pragma once
+
+#include "common.hpp"
+
+namespace msbfs {
+namespace bp {
+
+// build the bottom-up active lists (deg > 0, not done) over the vertices v = part + i*nparts,
+// i < cnt, split by degree (nparts = 1: every vertex; the hybrid mode's vertex-partitioned
+// level pulls only for its own residue class)
+template <int QCAP>
+__global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, int nparts,
+                                                         const int64_t* rowptr,
+                                                         const uint32_t* done, int wide_deg,
+                                                         int32_t* act, int32_t* actw, Ctr* ctr) {
+  // Each block owns QCAP consecutive list positions j and flushes its narrow queue once at the
+  // end (one counter atomic per QCAP vertices: atomics on one address serialise, and 64K of them
+  // were most of this kernel's time on 33M vertices). Blocks are dispatched in order, so the
+  // lists come out nearly ascending (hubs first in the wide list: the chunk kernel deals chunks
+  // in list order, and a grid-stride build that interleaved distant ranges cost ~1 ms of level-2
+  // tail on RMAT-26). The rare wide vertices go through a small queue flushed when needed.
+  constexpr int VPT = 4;  // vertices per thread per step (loads first, pushes after)
+  constexpr int64_t kStep = (int64_t)VPT * kBlock;
+  static_assert(QCAP % kStep == 0, "whole steps per block");
+  __shared__ LdsQueueN<QCAP> qn;
+  __shared__ LdsQueue qw;
+  __shared__ unsigned long long scratch[kWaves];
+  q_init(qn);
+  q_init(qw);
+  __syncthreads();
+  unsigned long long eu = 0;
+  const int64_t b0 = (int64_t)blockIdx.x * QCAP, b1 = min(b0 + (int64_t)QCAP, cnt);
+  for (int64_t b = b0; b < b1; b += kStep) {
+    int64_t d[VPT];
+    uint32_t dw[VPT];
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int64_t j = b + q * kBlock + threadIdx.x;
+      const int64_t i = part + j * nparts;
+      d[q] = 0;
+      dw[q] = ~0u;
+      if (j < b1) {
+        d[q] = rowptr[i + 1] - rowptr[i];
+        dw[q] = done[i >> 5];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int64_t i = part + (b + q * kBlock + threadIdx.x) * nparts;
+      const bool ok = d[q] > 0 && !((dw[q] >> (i & 31)) & 1u);
+      if (ok) eu += (unsigned long long)d[q];
+      q_push(qn, ok && d[q] <= wide_deg, (int32_t)i);
+      q_push(qw, ok && d[q] > wide_deg, (int32_t)i);
+    }
+    q_flush(qw, actw, &ctr->actw2.v, (int)kStep, false);
+  }
+  q_flush(qn, act, &ctr->act2.v, 0, true);
+  q_flush(qw, actw, &ctr->actw2.v, 0, true);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sparse row codes for the first bottom-up level. Its frontier is the level-1 frontier: outside
+// the top hubs a vertex there was reached from one or two sources, so its visited row (8*W bytes)
+// mostly holds a single set bit (RMAT-26, 1024 groups: ~1.2 bits per row below degree ~9K).
+// Gathering those rows made the level bound by Infinity-Cache traffic (rocprofv3, k_bu_chunks at
+// level 2: 44 % L2 hit rate, ~115 GB of L2 misses for 0.74e9 row gathers). code[u] (32 bit):
+// 0 = row empty; else bits 30-31 = number of set groups c (1-3) and bits 10*i .. 10*i+9 their
+// ids (groups < 1024); kDenseCode = anything else (gathered as before). Several slots: the
+// multi-bit rows of the mid-degree ids (RMAT-26: degree 1K-8K, 1-2 expected bits) were most of
+// the level's L2 misses (the dense rows left did not fit one XCD's 4 MB L2 next to the top hubs'
+// rows; single-slot codes 7.5 ms for the level's chunk pulls, two slots 6.9 ms). The
+// frontier's codes occupy a 64x smaller footprint than its rows, so the pulls mostly hit L2.
+// Only ids >= code_from use codes: after degree relabelling the lower ids are the hubs, whose rows
+// are dense and L2-resident. The codes live in the top-down touched buffer (unused by bottom-up
+// levels, rebuilt by every top-down level).
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kDenseCode = 0xFFFFFFFFu;  // (3 slots of group 1023: never a real code)
+constexpr int kCodeSlots = 3;
+// group of slot i of a sparse code, -1 for an unused slot
+__device__ __forceinline__ int code_g(uint32_t c, int i) {
+  return i < (int)(c >> 30) ? (int)((c >> (10 * i)) & 1023u) : -1;
+}
+constexpr int32_t kNoCodes = INT32_MAX;
+
+template <int W>
+// ids [lo, hi), then the list entries fl[0..nl) >= hi
+__global__ __launch_bounds__(kBlock) void k_build_codes(const uint64_t* R, const uint32_t* anyvis,
+                                                        int64_t lo, int64_t hi, const int32_t* fl,
+                                                        int64_t nl, uint32_t* code) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < hi - lo + nl;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t u = i < hi - lo ? lo + i : (int64_t)fl[i - (hi - lo)];
+    if (i >= hi - lo && u < hi) continue;
+    uint32_t c = 0;
+    if (any_visited(anyvis, (int32_t)u)) {
+      int pc = 0;
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        uint64_t w = R[u * W + j];
+        const int pw = __popcll(w);
+        if (pc + pw <= kCodeSlots) {  // (dense hub rows skip the bit loop)
+          while (w) {
+            const int b = __ffsll((unsigned long long)w) - 1;
+            w &= w - 1;
+            c |= (uint32_t)(j * 64 + b) << (10 * pc);
+            ++pc;
+          }
+        } else {
+          pc += pw;
+        }
+      }
+      c = pc == 0 ? 0u : pc <= kCodeSlots ? c | ((uint32_t)pc << 30) : kDenseCode;
+    }
+    code[u] = c;
+  }
+}
+
+// first id with degree < min_deg (rows relabelled by descending degree; one thread)
+__global__ void k_degree_bound(const int64_t* rowptr, int64_t n, int64_t min_deg, int32_t* out) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rowptr[mid + 1] - rowptr[mid] < min_deg) hi = mid;
+    else lo = mid + 1;
+  }
+  *out = (int32_t)lo;
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Prefix pull + tail push for the first bottom-up level (rows sorted by id, degree relabelled).
+// The LDS hub bitmap covers the ids < H; a pull that scanned whole rows had to probe the global
+// visited bitmap for every neighbour id >= H (the degree tail: ~40 % of the edge endpoints on
+// RMAT-26, almost none of them in the level-1 frontier). Instead the pulls stop at the first id
+// >= H, and the few level-1 frontier vertices u >= H push their bits to their neighbours here:
+// acc[v] |= row(u) (atomicOr, mostly one word thanks to the sparse codes) and stamp[v] = epoch.
+// The narrow pull folds acc[v] of stamped vertices into its accumulator (and clears it); wide
+// vertices collect it with their chunk results in k_bu_wide_finalize. Sources need no push:
+// every neighbour of a source was reached at level 1. Only own vertices (v % nparts == part) are
+// targets (the hybrid mode's level 2 pulls only those), and done vertices are skipped, so every
+// written acc entry is consumed and cleared within the level.
+// ---------------------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_push_tail(
+    const int32_t* fl, int64_t nf, int32_t H, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, const uint32_t* code, int32_t code_from, const uint32_t* done,
+    int part, int nparts, uint64_t* acc, int32_t* stamp, int32_t epoch) {
+  // 16 lanes per frontier entry, 4 entries per wave in flight (tail vertices have tens to a few
+  // hundred neighbours; the lanes of an entry take consecutive row entries)
+  constexpr int PG = 64;
+  const int lane = lane_id(), slot = lane % PG;
+  const int64_t grp = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / PG;
+  const int64_t ngrp = ((int64_t)gridDim.x * kBlock) / PG;
+  for (int64_t i = grp; i < nf; i += ngrp) {
+    const int32_t u = fl[i];
+    if (u < H) continue;
+    const uint32_t c = (code && u >= code_from) ? code[u] : kDenseCode;
+    if (c == 0) continue;
+    const int64_t b = rowptr[u], e = rowptr[u + 1];
+    for (int64_t k = b + slot; k < e; k += PG) {
+      const int32_t v = col[k];
+      if (nparts > 1 && v % nparts != part) continue;
+      if (is_done(done, v)) continue;
+      if (c != kDenseCode) {
+        for (int i = 0; i < kCodeSlots; ++i) {
+          const int g = code_g(c, i);
+          if (g >= 0) atomicOr((unsigned long long*)&acc[(int64_t)v * W + (g >> 6)], 1ull << (g & 63));
+        }
+      } else {
+        for (int j = 0; j < W; ++j) {
+          const uint64_t w = R[(int64_t)u * W + j];
+          if (w) atomicOr((unsigned long long*)&acc[(int64_t)v * W + j], (unsigned long long)w);
+        }
+      }
+      stamp[v] = epoch;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// bottom-up, narrow vertices: G lanes per vertex, early exit when every alive group is covered.
+// Each step takes C = 8 neighbours: the group's G lanes load and filter them cooperatively
+// (8/G column ids + 8/G bitmap probes per lane instead of 8 + 8), then every lane pulls its
+// slot of each surviving neighbour's row (ids broadcast inside the group by shuffles).
+// BT = block size; HUBW > 0: probes of the HUBW*32 lowest ids (hubs) read an LDS snapshot of
+// the visited bitmap (see k_bu_chunks; big blocks amortise the copy).
+// ---------------------------------------------------------------------------------------------
+//
+// FUSE: the level's new-bit counts are accumulated here (register bit-sliced counters -> LDS ->
+// this block's row of the counter slab, slabF = first row of this launch) instead of by a
+// separate k_count_frontier pass that re-reads both rows of every new frontier vertex.
+// PFX (prefix-pull level, see k_push_tail): rows are scanned only up to the first id >= HUBW*32,
+// and pushed bits (acc of vertices with stamp == epoch) seed the accumulator.
+// CS = neighbours per step (rows gathered between two coverage checks).
+// C1 > 0 (unfiltered levels only): a first step of just C1 rows before the CS-wide steps; late
+// levels are mostly covered by the first neighbour or two (sorted rows: hubs first).
+template <int W, bool COUNT, int BT, int HUBW, bool FUSE, bool FILT = true, bool PFX = false,
+          int CS = 8, int C1 = 0, int MINW = 4>
+__global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
+    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
+    int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
+    int next_wide, uint32_t* slabF, uint64_t* pacc, const int32_t* stamp, int32_t epoch,
+    const int32_t* plen, const uint32_t* nact_dev, const uint32_t* snap) {
+  static_assert(!PFX || HUBW > 0, "the prefix pull relies on the LDS hub bitmap");
+  // snap (first pull level of a batch that did not clear its visited buffer, see start_batch):
+  // the any-visited bitmap as of the level start. Probes read it (a vertex first visited during
+  // this level may still have a stale row) and an own row it does not mark is all zero.
+  const uint32_t* pvis = snap ? snap : anyvis;
+  if (nact_dev) nact = (int64_t)*nact_dev;  // (list length known only on the device)
+  static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
+  constexpr int NWV = BT / 64, TILE = NWV * VPW;
+  constexpr int C = CS;                      // neighbours per step
+  constexpr int Q = C / G > 0 ? C / G : 1;   // ids loaded per lane per step
+  static_assert(G * Q == C || (C < G && Q == 1), "step = whole lane groups or part of one");
+  __shared__ LdsQueue qa, qf, qw;
+  __shared__ unsigned long long scratch[NWV];
+  __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
+  // counter rows of CR words per 64 groups, bank-skewed (see BitCounter::spill_strided) except
+  // on the prefix level: its sparse spills ran level 2 ~0.2 ms slower skewed (4 runs each)
+  constexpr int CR = PFX ? 64 : 65;
+  __shared__ uint32_t cnt[FUSE ? CR * W : 1];
+  if constexpr (HUBW > 0)
+    for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = pvis[i];
+  if constexpr (FUSE)
+    for (int i = threadIdx.x; i < CR * W; i += BT) cnt[i] = 0;
+  q_init(qa);
+  q_init(qf);
+  q_init(qw);
+  __syncthreads();
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  unsigned long long eu = 0, ef = 0, ev = 0;
+  BitCounter<VW, PFX ? 5 : 6> bc;
+  int nadd = 0;
+  if constexpr (FUSE) bc.zero();
+  // Software pipeline over the grid-stride tiles: the active-list entry is loaded two tiles
+  // ahead and the vertex's visited row and row offsets one tile ahead, so a tile starts with
+  // its column loads instead of two dependent round trips (list entry -> row / offsets).
+  const int64_t stride = (int64_t)gridDim.x * TILE, lofs = wv * VPW + sub;
+  int64_t tb = (int64_t)blockIdx.x * TILE;
+  int32_t v1 = 0, v2 = 0;  // list entries of tiles tb and tb + stride
+  V<VW> r1 = vzero<VW>();  // row of v1
+  int64_t b1 = 0;          // row offsets of v1
+  uint32_t d1 = 0;
+  if (tb + lofs < nact) v1 = act[tb + lofs];
+  if (tb + stride + lofs < nact) v2 = act[tb + stride + lofs];
+  uint32_t p1 = 0;  // PFX: prefix length of v1's row (ids < H)
+  if (tb + lofs < nact) {
+    r1 = (snap && !any_visited(snap, v1)) ? vzero<VW>() : ldv<VW>(R + (int64_t)v1 * W + slot * VW);
+    b1 = rowptr[v1];
+    d1 = (uint32_t)(rowptr[v1 + 1] - b1);
+    if constexpr (PFX) p1 = (uint32_t)plen[v1];
+  }
+  int32_t u1[Q];  // first-step column ids of the current tile's vertex (third pipeline stage)
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    u1[q] = (tb + lofs < nact && q * G + slot < C && (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
+                ? col[b1 + q * G + slot] : -1;
+  for (; tb < nact; tb += stride) {
+    const int64_t idx = tb + lofs;
+    const bool valid = idx < nact;
+    const int32_t v = valid ? v1 : 0;
+    const V<VW> r = r1;
+    const int64_t beg = b1, end = b1 + (PFX ? p1 : d1);  // PFX: pull only the prefix
+    const uint32_t deg = d1;
+    int32_t u0[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) u0[q] = u1[q];
+    // prefetch: row / offsets of the next tile, list entry of the one after
+    v1 = v2;
+    if (idx + stride < nact) {
+      r1 = (snap && !any_visited(snap, v1)) ? vzero<VW>() : ldv<VW>(R + (int64_t)v1 * W + slot * VW);
+      b1 = rowptr[v1];
+      d1 = (uint32_t)(rowptr[v1 + 1] - b1);
+      if constexpr (PFX) p1 = (uint32_t)plen[v1];
+    }
+    if (idx + 2 * stride < nact) v2 = act[idx + 2 * stride];
+    V<VW> unv = vzero<VW>(), acc = vzero<VW>();
+    bool lane_open = false, rnz = false;
+    if (valid) {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        unv.w[j] = ~r.w[j] & am.w[j];
+        lane_open |= unv.w[j] != 0;
+        rnz |= r.w[j] != 0;
+      }
+    }
+    if constexpr (PFX) {  // bits pushed from the tail frontier (k_push_tail)
+      if (valid && stamp[v] == epoch) {
+        acc = ldv<VW>(pacc + (int64_t)v * W + slot * VW);
+        stv<VW>(pacc + (int64_t)v * W + slot * VW, vzero<VW>());
+      }
+    }
+    const bool g_open = valid && ((__ballot(lane_open) >> (sub * G)) & L::GBITS);
+    int64_t e0 = beg;
+    bool g_cov = false;
+    if constexpr (C1 > 0) {
+      static_assert(!FILT, "the short first step skips the filter");
+      if (g_open) {
+        V<VW> x[C1];
+#pragma unroll
+        for (int c = 0; c < C1; ++c) {
+          const int32_t uc = G == 1 ? u0[c] : __shfl(u0[c / G], sub * G + (c % G));
+          x[c] = uc >= 0 ? ldv<VW>(R + (int64_t)uc * W + slot * VW) : vzero<VW>();
+        }
+        bool cov = true;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+#pragma unroll
+          for (int c = 0; c < C1; ++c) acc.w[j] |= x[c].w[j];
+          cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
+        }
+        g_cov = !((__ballot(!cov) >> (sub * G)) & L::GBITS);
+        e0 = beg + C1;
+      }
+    }
+    if (g_open && !g_cov) {
+      for (int64_t e = e0; e < end; e += C) {
+        int32_t u[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int64_t ee = e + q * G + slot;
+          // first step: preloaded (without the short first step)
+          u[q] = (C1 == 0 && e == beg) ? u0[q]
+                                       : ((q * G + slot < C && ee < end) ? col[ee] : -1);
+        }
+
+        // ids below filter_from are loaded without a probe (filter off: filter_from = INT_MAX)
+        // probes: every load first, every use after (with the use next to the load inside the
+        // branch the compiler waited for each probe before issuing the next)
+        if (FILT && filter_from != INT32_MAX) {  // wave-uniform
+          // (LDS and global results in separate registers: a shared destination made the LDS
+          // read wait for the outstanding global probes)
+          uint32_t pg[Q], ph[Q];
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            pg[q] = ~0u;
+            if (u[q] >= filter_from && !(HUBW > 0 && u[q] < HUBW * 32)) pg[q] = pvis[u[q] >> 5];
+          }
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            ph[q] = ~0u;
+            if (HUBW > 0 && u[q] >= filter_from && u[q] < HUBW * 32) ph[q] = hub[u[q] >> 5];
+          }
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (!(((pg[q] & ph[q]) >> (u[q] & 31)) & 1u)) u[q] = -1;
+        }
+        V<VW> x[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          // candidate c = column entry e + c: lane (c % G) of this group holds it in u[c / G]
+          const int32_t uc = G == 1 ? u[c] : __shfl(u[c / G], sub * G + (c % G));
+          x[c] = uc >= 0 ? ldv<VW>(R + (int64_t)uc * W + slot * VW) : vzero<VW>();
+        }
+        bool cov = true;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+#pragma unroll
+          for (int c = 0; c < C; ++c) acc.w[j] |= x[c].w[j];
+          cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
+        }
+        // the whole group runs this loop in lock step (same v); exit when all lanes covered
+        if (!((__ballot(!cov) >> (sub * G)) & L::GBITS)) break;
+
+      }
+    }
+    V<VW> nw;
+    bool anynew = false, notfull = false;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      nw.w[j] = acc.w[j] & unv.w[j];
+      anynew |= nw.w[j] != 0;
+      notfull |= (unv.w[j] & ~nw.w[j]) != 0;
+    }
+    if (valid) {  // also when nothing is open: Wb may hold the previous batch's rows
+      V<VW> nv;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
+      stv<VW>(Wb + (int64_t)v * W + slot * VW, nv);
+    }
+    if constexpr (FUSE) {  // nw is zero for invalid lanes
+      bc.add(nw);
+      if (++nadd == (1 << BitCounter<VW, PFX ? 5 : 6>::D) - 1) {
+        bc.template spill_strided<CR>(cnt, slot);
+        nadd = 0;
+      }
+    }
+    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
+    const bool g_new = (bn >> (sub * G)) & L::GBITS;
+    const bool g_nf = (bf >> (sub * G)) & L::GBITS;
+    const bool leader = valid && slot == 0;
+    if (leader && !g_nf) set_done(done, v);
+    const bool keep = leader && g_nf, app = leader && g_new;
+    if (keep) eu += deg;
+    if (app) ef += deg;
+    {
+      const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
+      if (leader && g_first) {
+        atomicOr(&anyvis[v >> 5], 1u << (v & 31));
+        ev += deg;
+      }
+    }
+    // third stage: the next tile's first-step ids (its offsets arrived during this tile)
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      u1[q] = (idx + stride < nact && q * G + slot < C &&
+               (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
+                  ? col[b1 + q * G + slot] : -1;
+    q_push(qa, keep && (int)deg <= next_wide, v);
+    q_push(qw, keep && (int)deg > next_wide, v);
+    q_push(qf, app, v);
+    q_flush(qa, act2, &ctr->act2.v, TILE, false);
+    q_flush(qw, actw2, &ctr->actw2.v, TILE, false);
+    q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
+  }
+  q_flush(qa, act2, &ctr->act2.v, 0, true);
+  q_flush(qw, actw2, &ctr->actw2.v, 0, true);
+  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
+  if constexpr (FUSE) {
+    bc.template spill_strided<CR>(cnt, slot);
+    __syncthreads();
+    uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+    for (int i = threadIdx.x; i < 64 * W; i += BT) row[i] = cnt[CR == 65 ? i + (i >> 6) : i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Late pull levels, first pass: from the third bottom-up level on almost every
+// active vertex is covered by its first neighbour (rows sorted: the biggest hub first), and the
+// level is bound by the latency of its dependent loads (list entry -> row offsets -> first column
+// id -> neighbour row). This lean kernel (no multi-step loop, no software pipeline) keeps few
+// registers, so twice as many waves hide that latency. A vertex the first row covers is
+// finished here exactly as k_bu_narrow would (row, counts, done bit, frontier, anyvis); the others
+// go to an overflow list (ctr->touched, unused by pull levels) that k_bu_narrow then processes
+// from scratch.
+// ---------------------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(kBlock, 8) void k_bu_first(
+    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
+    int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF, const int32_t* first) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  constexpr int CR = 65;  // bank-skewed counter rows (see BitCounter::spill_strided)
+  __shared__ LdsQueue qo, qf;
+  __shared__ unsigned long long scratch[kWaves];
+  __shared__ uint32_t cnt[CR * W];
+  for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
+  q_init(qo);
+  q_init(qf);
+  __syncthreads();
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  unsigned long long ef = 0, ev = 0;
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nact; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t idx = tb + wv * VPW + sub;
+    const bool valid = idx < nact;
+    int32_t v = 0;
+    V<VW> r = vzero<VW>(), nw = vzero<VW>();
+    uint32_t deg = 0;
+    bool open = false, rnz = false;
+    if (valid) {
+      v = act[idx];
+      const int32_t u = first ? first[v] : col[rowptr[v]];  // active vertices have deg > 0
+      r = ldv<VW>(R + (int64_t)v * W + slot * VW);
+      deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);  // only counted, off the load chain
+      const V<VW> x = ldv<VW>(R + (int64_t)u * W + slot * VW);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        const uint64_t unv = ~r.w[j] & am.w[j];
+        nw.w[j] = x.w[j] & unv;
+        open |= (unv & ~nw.w[j]) != 0;
+        rnz |= r.w[j] != 0;
+      }
+    }
+    const bool g_open = (__ballot(open) >> (sub * G)) & L::GBITS;
+    const bool fin = valid && !g_open;  // covered by the first row: finished at this level
+    if (!fin) nw = vzero<VW>();
+    if (fin) {
+      V<VW> nv;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
+      stv<VW>(Wb + (int64_t)v * W + slot * VW, nv);
+    }
+    bc.add(nw);
+    if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+      bc.template spill_strided<CR>(cnt, slot);
+      nadd = 0;
+    }
+    bool anynew = false;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) anynew |= nw.w[j] != 0;
+    const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
+    const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
+    const bool leader = valid && slot == 0;
+    if (leader && fin) set_done(done, v);
+    if (leader && g_new) ef += deg;
+    if (leader && g_first) {
+      atomicOr(&anyvis[v >> 5], 1u << (v & 31));
+      ev += deg;
+    }
+    q_push(qo, leader && !fin, v);
+    q_push(qf, leader && g_new, v);
+    q_flush(qo, ovf, &ctr->touched.v, TILE, false);
+    q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
+  }
+  q_flush(qo, ovf, &ctr->touched.v, 0, true);
+  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
+  bc.template spill_strided<CR>(cnt, slot);
+  __syncthreads();
+  uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+  for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
+}
+
+// bottom-up, wide vertices, phase 1: one wave per edge chunk (<= kChunk edges), processed in
+// tiles of 256 edges so the dependent loads are batched instead of chained per neighbour:
+//   A) all 64 lanes load 4 column ids each (one coalesced 1-KB pass), optionally test them
+//      against the visited-by-anyone bitmap (256 independent loads), and compact the survivors
+//      into an LDS list (ballot + popcount prefix);
+//   B) the S = 64/G lane groups pull 4 neighbour rows each per step (4*S rows in flight per
+//      wave), OR-reduce across groups (xor shuffles) and stop once every alive group is covered.
+// The chunk's new bits are merged into acc[v] with atomicOr (k_bu_wide_finalize folds them in).
+// offs = inclusive prefix of chunk counts over the wide list.
+//
+// HUBW > 0 (levels that filter): the block first copies the visited bitmap of the HUBW*32
+// lowest ids into LDS. After degree relabelling those are the hubs, which carry most edge
+// endpoints (RMAT-26: the top 2^19 ids take roughly two thirds), so most filter probes become
+// LDS reads instead of divergent global loads. The copy is a snapshot taken at kernel start; a
+// bit another kernel of this level sets later belongs to a vertex first visited at this level,
+// whose row in R is still zero, so skipping it is exact. Big blocks (BT threads, 2 per CU)
+// amortise the copy; the grid is persistent (grid-stride over chunks).
+// One wave pulls edges [beg, lim) of wide vertex v (a chunk) and publishes the new bits into
+// acc[v] (k_bu_wide_finalize folds them in). coop: chunks of one vertex run concurrently and
+// share progress through acc (see below); coop = 0 (first bottom-up level) skips that.
+template <int W, int T, int HUBW>
+__device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, const int32_t* col,
+                                           const uint64_t* R, const V<Lay<W>::VW>& am,
+                                           uint64_t* acc, const uint32_t* anyvis,
+                                           const uint32_t* hub, int32_t filter_from, int coop,
+                                           int32_t* lst, const uint32_t* code,
+                                           int32_t code_from, unsigned long long* wacc,
+                                           const uint32_t* snap) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, S = L::VPW;
+  constexpr int PB = VW == 2 ? 4 : 8;  // rows in flight per lane group in phase B
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int64_t vo = (int64_t)v * W + slot * VW;
+  const V<VW> r = (snap && !any_visited(snap, v)) ? vzero<VW>() : ldv<VW>(R + vo);  // see k_bu_narrow
+  // g = bits the vertex's other chunks have published so far. Chunks of one hub run
+  // concurrently, so each tile publishes its partial OR with a RETURNING atomicOr that also
+  // hands back the current union from the memory side (atomics bypass the non-coherent per-XCD
+  // L2s); every chunk stops once the union covers all alive groups.
+  V<VW> g = vzero<VW>();
+  if (coop) {
+    if (sub == 0) {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) g.w[j] = atomicOr((unsigned long long*)&acc[vo + j], 0ull);
+    }
+#pragma unroll
+    for (int j = 0; j < VW; ++j) g.w[j] = __shfl(g.w[j], slot);  // lane slot of sub-group 0
+  }
+  V<VW> unv, a = vzero<VW>();
+  bool lane_open = false;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    unv.w[j] = ~r.w[j] & am.w[j];
+    lane_open |= (unv.w[j] & ~g.w[j]) != 0;
+  }
+  if (!__ballot(lane_open)) return;  // wave-uniform
+  bool covered = false;
+  for (int64_t t0 = beg; t0 < lim && !covered; t0 += T) {
+    // ---- phase A: ids of this tile, filtered, compacted into lst[0..cnt)
+    constexpr int Q = T / 64;
+    int32_t u[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int64_t e = t0 + q * 64 + lane;
+      u[q] = e < lim ? col[e] : -1;
+    }
+    if (filter_from != INT32_MAX) {
+      // probes: every load first, every use after (see k_bu_narrow)
+      uint32_t pg[Q], ph[Q];  // separate destinations (see k_bu_narrow)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        pg[q] = ~0u;
+        if (u[q] >= filter_from && !(HUBW > 0 && u[q] < HUBW * 32)) pg[q] = anyvis[u[q] >> 5];
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        ph[q] = ~0u;
+        if (HUBW > 0 && u[q] >= 0 && u[q] < HUBW * 32) ph[q] = hub[u[q] >> 5];
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (u[q] >= 0 && !(((pg[q] & ph[q]) >> (u[q] & 31)) & 1u)) u[q] = -1;
+    }
+    if (code_from != kNoCodes) {  // wave-uniform
+      // single-group neighbours: their bit goes into this wave's LDS words (ds_or_b64) instead
+      // of a row gather; the words are folded into every lane group's accumulator below
+      if (lane < W) wacc[lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      uint32_t cd[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        cd[q] = kDenseCode;
+        if (u[q] >= code_from) cd[q] = code[u[q]];
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (cd[q] != kDenseCode) {
+#pragma unroll
+          for (int i = 0; i < kCodeSlots; ++i) {
+            const int g = code_g(cd[q], i);
+            if (g >= 0) atomicOr(&wacc[g >> 6], 1ull << (g & 63));
+          }
+          u[q] = -1;
+        }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < VW; ++j) a.w[j] |= wacc[slot * VW + j];
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint64_t m = __ballot(u[q] >= 0);
+      if (u[q] >= 0) lst[cnt + __popcll(m & lanemask_lt())] = u[q];
+      cnt += __popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- phase B: rows of the surviving neighbours, PB per lane group per step
+    for (int b = 0; b < cnt; b += PB * S) {
+      int32_t uu[PB];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int k = b + q * S + sub;
+        uu[q] = k < cnt ? lst[k] : -1;
+      }
+      {
+        // loads first, ORs after: the compiler then keeps all PB loads in flight
+        V<VW> x[PB];
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+          x[q] = vzero<VW>();
+          if (uu[q] >= 0) x[q] = ldv<VW>(R + (int64_t)uu[q] * W + slot * VW);
+        }
+#pragma unroll
+        for (int q = 0; q < PB; ++q)
+#pragma unroll
+          for (int j = 0; j < VW; ++j) a.w[j] |= x[q].w[j];
+      }
+#pragma unroll
+      for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+        for (int j = 0; j < VW; ++j) a.w[j] |= __shfl_xor(a.w[j], off);
+      bool cov = true;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
+      if (!__ballot(!cov)) {
+        covered = true;
+        break;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // lst is rewritten by the next tile
+    // publish this chunk's bits so far and pick up the other chunks' (one round trip)
+    if (coop && !covered && t0 + T < lim) {
+      bool cov = true;
+      if (sub == 0) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          const uint64_t nb = a.w[j] & unv.w[j] & ~g.w[j];
+          g.w[j] |= nb ? atomicOr((unsigned long long*)&acc[vo + j], nb)
+                       : atomicOr((unsigned long long*)&acc[vo + j], 0ull);
+          g.w[j] |= nb;
+          cov &= ((a.w[j] | g.w[j]) & unv.w[j]) == unv.w[j];
+        }
+      }
+      if (!__ballot(!cov)) covered = true;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) g.w[j] = __shfl(g.w[j], slot);
+    }
+  }
+  if (sub == 0) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const uint64_t nb = a.w[j] & unv.w[j] & ~g.w[j];
+      if (nb) atomicOr((unsigned long long*)&acc[vo + j], nb);
+    }
+  }
+}
+
+// Chunk descriptor: vertex, first column position, edge count (<= kChunk). Built once per level
+// by k_chunk_desc; a wave reads its next descriptor with one scalar load while it pulls the
+// current chunk (vs an owner -> list entry -> row offsets chain of dependent loads per chunk).
+struct ChunkDesc {
+  int32_t v;
+  uint32_t beg_lo, beg_hi;
+  int32_t len;
+};
+
+// first position in the sorted row [b, e) whose id is >= H
+__device__ __forceinline__ int64_t row_lower_bound(const int32_t* col, int64_t b, int64_t e,
+                                                   int32_t H) {
+  while (b < e) {
+    const int64_t mid = (b + e) >> 1;
+    if (col[mid] < H) b = mid + 1;
+    else e = mid;
+  }
+  return b;
+}
+
+// plen[v] = length of v's row prefix with ids < H (rows sorted; a graph property, computed once
+// per graph and bound H, see BitparSolver::prefix_lens)
+__global__ __launch_bounds__(kBlock) void k_prefix_lens(const int64_t* rowptr, const int32_t* col,
+                                                        int64_t n, int32_t H, int32_t* plen) {
+  for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n;
+       v += (int64_t)gridDim.x * kBlock) {
+    const int64_t b = rowptr[v];
+    plen[v] = (int32_t)(row_lower_bound(col, b, rowptr[v + 1], H) - b);
+  }
+}
+
+// first[v] = v's first neighbour (rows sorted: after degree relabelling its biggest hub), -1 for
+// an isolated vertex: the lean first-row pass (k_bu_first) reads it with one coalesced 4-byte load
+// instead of the rowptr -> col chain, whose col[rowptr[v]] touches one 128-byte line per vertex
+__global__ __launch_bounds__(kBlock) void k_first_nbr(const int64_t* rowptr, const int32_t* col,
+                                                      int64_t n, int32_t* first) {
+  for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n;
+       v += (int64_t)gridDim.x * kBlock) {
+    const int64_t b = rowptr[v];
+    first[v] = rowptr[v + 1] > b ? col[b] : -1;
+  }
+}
+
+// chunk counts of the wide vertices' row prefixes (inclusive-scanned into offs by the host)
+__global__ __launch_bounds__(kBlock) void k_prefix_chunks(const int32_t* wl, int64_t nw,
+                                                          const int32_t* plen, int64_t* cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
+       i += (int64_t)gridDim.x * kBlock)
+    cnt[i] = ((int64_t)plen[wl[i]] + kChunk - 1) / kChunk;
+}
+
+// plen != nullptr: chunks cover only the row prefixes with ids < H (prefix-pull level)
+__global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl, int64_t nw,
+                                                       const int64_t* offs, const int64_t* rowptr,
+                                                       const int32_t* plen, ChunkDesc* desc) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int32_t v = wl[i];
+    const int64_t b = rowptr[v];
+    const int64_t e = plen ? b + plen[v] : rowptr[v + 1];
+    const int64_t c0 = i ? offs[i - 1] : 0, c1 = offs[i];
+    for (int64_t c = c0; c < c1; ++c) {
+      const int64_t cb = b + (c - c0) * kChunk;
+      desc[c] = ChunkDesc{v, (uint32_t)cb, (uint32_t)((uint64_t)cb >> 32),
+                          (int32_t)min((int64_t)kChunk, e - cb)};
+    }
+  }
+}
+
+template <int W, int T, int BT, int HUBW>
+__global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_bu_chunks(
+    const ChunkDesc* __restrict__ desc, const int64_t* nchunks_p, const int32_t* col,
+    const uint64_t* R,
+    const uint64_t* alive, const uint64_t* gmask, uint64_t* acc, const uint32_t* anyvis,
+    int32_t filter_from, int coop, const uint32_t* code, int32_t code_from,
+    const uint32_t* snap) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G;
+  __shared__ int32_t tile[BT / 64][T];
+  __shared__ unsigned long long wacc[BT / 64][W];
+  __shared__ uint32_t hub[HUBW > 0 ? HUBW : 1];
+  if (snap) anyvis = snap;  // probes read the level-start bitmap (see k_bu_narrow)
+  if constexpr (HUBW > 0) {
+    for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = anyvis[i];
+    __syncthreads();
+  }
+  const int slot = lane_id() % G;
+  int32_t* lst = tile[threadIdx.x >> 6];
+  const int64_t nchunks = uni64(*nchunks_p);  // inclusive chunk prefix of the last wide vertex
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  // Chunk order. Without early exit (coop = 0: the first bottom-up level, where hardly any row
+  // is covered) chunks are dealt round robin over the waves, which balances the hubs' expensive
+  // chunks. With early exit a wave takes a contiguous run, so a vertex's later chunks usually
+  // come after its earlier ones have published their bits and are skipped at the first check.
+  const int64_t cstart = uni64(coop ? nchunks * wave / nwaves : wave);
+  const int64_t cend = uni64(coop ? nchunks * (wave + 1) / nwaves : nchunks);
+  const int64_t cstep = uni64(coop ? 1 : nwaves);
+  ChunkDesc d{0, 0, 0, 0};
+  if (cstart < cend) d = desc[cstart];
+  for (int64_t c = cstart; c < cend; c += cstep) {
+    const int32_t v = uni32(d.v);
+    const int64_t beg = uni64((int64_t)(((uint64_t)d.beg_hi << 32) | d.beg_lo));
+    const int64_t lim = beg + uni32(d.len);
+    if (c + cstep < cend) d = desc[c + cstep];  // next descriptor, in flight during the pull
+    chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop,
+                           lst, code, code_from, wacc[threadIdx.x >> 6], snap);
+  }
+}
+
+// bottom-up, wide vertices, phase 2: G lanes per vertex fold acc[v] into the visited words.
+template <int W, bool COUNT, bool FUSE>
+__global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
+    const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, uint64_t* Wb,
+    uint64_t* acc, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* actw2,
+    int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* act2n, int next_wide, uint32_t* slabF,
+    const uint32_t* snap) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  __shared__ LdsQueue qa, qf, qn;
+  __shared__ unsigned long long scratch[kWaves];
+  // bank-skewed counter rows (see BitCounter::spill_strided): wide vertices gain many groups
+  // at once, so every spill touches most counters
+  constexpr int CR = 65;
+  __shared__ uint32_t cnt[FUSE ? CR * W : 1];
+  if constexpr (FUSE)
+    for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
+  q_init(qa);
+  q_init(qf);
+  q_init(qn);
+  __syncthreads();
+  BitCounter<VW> bc;
+  int nadd = 0;
+  if constexpr (FUSE) bc.zero();
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  unsigned long long eu = 0, ef = 0, ev = 0;
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nw; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t idx = tb + wv * VPW + sub;
+    const bool valid = idx < nw;
+    int32_t v = 0;
+    V<VW> nwb = vzero<VW>();
+    bool anynew = false, notfull = false, rnz = false;
+    uint32_t deg = 0;
+    if (valid) {
+      v = wl[idx];
+      const int64_t vo = (int64_t)v * W + slot * VW;
+      const V<VW> r = (snap && !any_visited(snap, v)) ? vzero<VW>() : ldv<VW>(R + vo);
+      const V<VW> a = ldv<VW>(acc + vo);
+      V<VW> nv;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        const uint64_t unv = ~r.w[j] & am.w[j];
+        nwb.w[j] = a.w[j] & unv;
+        nv.w[j] = r.w[j] | nwb.w[j];
+        anynew |= nwb.w[j] != 0;
+        notfull |= (unv & ~nwb.w[j]) != 0;
+        rnz |= r.w[j] != 0;
+      }
+      stv<VW>(acc + vo, vzero<VW>());
+      stv<VW>(Wb + vo, nv);
+      deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
+    }
+    if constexpr (FUSE) {  // nwb is zero for invalid lanes
+      bc.add(nwb);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.template spill_strided<CR>(cnt, slot);
+        nadd = 0;
+      }
+    }
+    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
+    const bool g_new = (bn >> (sub * G)) & L::GBITS;
+    const bool g_nf = (bf >> (sub * G)) & L::GBITS;
+    const bool leader = valid && slot == 0;
+    if (leader && !g_nf) set_done(done, v);
+    const bool keep = leader && g_nf, app = leader && g_new;
+    if (keep) eu += deg;
+    if (app) ef += deg;
+    {
+      const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
+      if (leader && g_first) {
+        atomicOr(&anyvis[v >> 5], 1u << (v & 31));
+        ev += deg;
+      }
+    }
+    q_push(qa, keep && (int)deg > next_wide, v);
+    q_push(qn, keep && (int)deg <= next_wide, v);
+    q_push(qf, app, v);
+    q_flush(qa, actw2, &ctr->actw2.v, TILE, false);
+    q_flush(qn, act2n, &ctr->act2.v, TILE, false);
+    q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
+  }
+  q_flush(qa, actw2, &ctr->actw2.v, 0, true);
+  q_flush(qn, act2n, &ctr->act2.v, 0, true);
+  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
+  if constexpr (FUSE) {
+    bc.template spill_strided<CR>(cnt, slot);
+    __syncthreads();
+    uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+    for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
+  }
+}
+
+}  // namespace bp
+}  // namespace msbfs

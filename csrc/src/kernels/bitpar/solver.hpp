@@ -1,0 +1,282 @@
+// Bit-parallel, direction-optimising multi-source BFS over up to 64*W query groups at once.
+//
+// What it replaces: the reference runs each query group as its own level-synchronous BFS with a
+// thread-per-vertex kernel that rescans all n distances every level (BFSKernal main.cu:16-38,
+// driven by GPUMultiSourceBFS main.cu:40-73), then copies all n distances to the host to sum them
+// (ComputeFofU main.cu:75-89). Queries run strictly one after another per rank
+// (main.cu:312-322).
+//
+// Here one pass over the graph advances 64*W groups together (MS-BFS, Then et al. VLDB'15):
+//  * every vertex owns W 64-bit words: bit k of word j = "visited by group 64j+k".
+//  * top-down levels (small frontiers) push frontier bits along edges with 64-bit atomicOr into
+//    an accumulator, edge-parallel via a load-balanced search over the frontier's degree prefix
+//    (no hub serialisation);
+//  * bottom-up levels (large frontiers) pull: an unfinished vertex ORs its neighbours' visited
+//    words and stops as soon as every still-alive group is covered (early exit). Double-buffered
+//    visited arrays make the pull race-free without a separate frontier array (a neighbour bit
+//    visited at any level <= L can only have been set exactly at L if it is still missing here).
+//    Low-degree vertices get G lanes each; high-degree vertices are cut into fixed-size edge
+//    chunks that many waves scan in parallel (partial ORs merged with atomicOr, then a finalize
+//    pass), so a 10^6-neighbour hub never serialises a level on one wave.
+//  * per-group F(U) = sum_level level * |newly visited| is accumulated on chip: every new bit adds
+//    to a per-group LDS counter; one global atomic per group per block at the end. Only 8 bytes
+//    per group ever leave the device (vs 4n bytes per query in the reference).
+//  * groups whose frontier died are masked out ("alive" words), so groups stuck in small
+//    components never stop other groups' vertices from finishing.
+//  * list building (active lists, frontiers, touched sets) goes through per-block LDS queues:
+//    one global atomic per ~1K items instead of one per wave (same-line atomics serialise).
+// Lane mapping for wave64: each lane owns VW (1-2) words = one 8-16 B load, a vertex's W words are
+// spread over G = W/VW consecutive lanes, so W=16 reads a vertex's 128-B line in one coalesced
+// wave-instruction slice.
+//
+// Source layout (one class, four translation units that compile in parallel):
+//   bitpar/common.hpp  init.hpp  push.hpp  pull.hpp  hybrid.hpp   kernels by family
+//   bitpar_solver.hip  construction, batches, the level loop (direction choice, reductions)
+//   bitpar_push.hip    top-down levels and the device-driven level batches
+//   bitpar_pull.hip    bottom-up levels (prefix pull + tail push, narrow / lean / chunk pulls)
+//   bitpar_hybrid.hip  the hybrid multi-GPU phases and the exchange coding
+#pragma once
+
+#include <chrono>
+#include <map>
+#include <memory>
+#include <string>
+
+#include "common.hpp"
+
+namespace msbfs {
+namespace bp {
+
+// Algorithm tuning of the bit-parallel solver. Defaults are the measured best (RMAT-26 / 1024
+// groups, RMAT-30, road grid, uniform graphs; see README). Set per solver through
+// Solver::tune ("key=value,key=value"; msbfs_solver_tune in the C API, Solver(tuning=...) in
+// Python) or process-wide through the one variable MSBFS_TUNE (same syntax; echoed on stderr).
+// Unknown keys and malformed values are errors, never ignored. Every key is exercised by a GPU
+// oracle test (tests/test_gpu_kernels.py).
+struct Tuning {
+  // push -> pull once the frontier's degree sum exceeds gamma x n_eff (0: off). Level 2, where
+  // the prefix pull applies, uses gamma2 (< 0: gamma): RMAT-30 / 16 groups 296 -> 106 ms
+  double gamma = 1.0, gamma2 = 0.25;
+  // first bottom-up level: 0 = whole-row pull; 2 = prefix pull (ids < 458752, the 56-KB LDS hub
+  // bitmap) + tail push (RMAT-26 level 2: 16.8 ms vs 21.2 for whole rows)
+  int pfx = 2;
+  // sparse single-group row codes on the first bottom-up level; ids with degree >=
+  // code_deg * nnz / (source degree sum), i.e. >= code_deg expected set bits, keep row gathers
+  int codes = 1;
+  double code_deg = 3.0;
+  // lean first-row pass on the third and later pull levels (k_bu_first) for active lists of at
+  // least lean_min vertices (RMAT-26 level 4: 2.48 -> 2.07 ms)
+  int lean = 1;
+  int64_t lean_min = 1 << 20;
+  int lazy = 1;        // no per-batch fill of the visited buffer (see start_batch)
+  int td_fused = 1;    // device-driven batches run the one-kernel k_td_fused levels
+  int64_t td_bm = 65536;  // k_td_fused walks the frontier bitmap from this frontier size on
+  int batch = 64;      // top-down levels per device-driven batch (1 = host-driven levels)
+  std::string dirs;    // forced per-level directions 'T'/'B' (tests, experiments)
+
+  void set(const std::string& key, const std::string& value);
+  void parse(const std::string& spec);  // "k=v,k=v"
+  static const Tuning& process_default();  // defaults + MSBFS_TUNE, read once per process
+};
+
+class BitparSolver final : public Solver {
+ public:
+  BitparSolver(const DeviceGraph& g, int max_groups);
+
+  void run(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t* F, int64_t* edges2,
+           RunStats* st, hipStream_t stream) override;
+  void tune(const std::string& spec) override { tun_.parse(spec); }
+
+  int64_t hybrid_max_groups() const override { return 64 * (int64_t)maxW_; }
+  void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,
+                      int64_t n_eff, bool count_l1, const int32_t* wbeg, uint64_t* send,
+                      int64_t* out, RunStats* st, hipStream_t s,
+                      int64_t* coded_len = nullptr) override;
+  void hybrid_phase_c(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
+                      const uint64_t* recv, const int64_t* reduced, int64_t* F_out, RunStats* st,
+                      hipStream_t s) override;
+  void hybrid_decode(const uint64_t* coded, const int64_t* coded_len, int nparts, int64_t n_eff,
+                     int w_count, uint64_t* dense, hipStream_t s) override;
+
+  // Level-loop state. The normal path runs one batch start to finish; the hybrid phases run
+  // a capped / range-restricted piece of it (phase A) or resume it from exchanged state (C).
+  struct Loop {
+    int cur = 0;  // vis_[cur] = read buffer (up to date for every non-done vertex)
+    int fc = 0;   // fl_[fc] = current frontier
+    int ac = 0;   // acc_[ac] holds the current frontier bits when fsrc_acc
+    int alv = 0;  // alive[alv] = groups with a non-empty frontier
+    uint32_t level = 0;
+    int64_t nf = 0, ef = 0, ev = 0, na = 0, ea = 0, nact = 0, nactw = 0;
+    bool have_active = false, fsrc_acc = true, bottom_up = false;
+    int bu_levels = 0;
+    // limits
+    uint32_t stop_level = 0xFFFFFFFFu;  // last level to run
+    int64_t cnt = 0;                    // first active-list build: v = part + i*nparts, i < cnt
+    int part = 0, nparts = 1;
+    bool weight_l1 = true;              // add level-1 counts to F
+    std::string plan;                   // plan[level] = 'T'/'B' forces the next level
+    int64_t ev_l1 = 0;                  // ev after level 1
+    int64_t ef0 = 0;                    // degree sum of the sources (level-0 frontier)
+    bool lazy = false;                  // no vis_[0] fill (see start_batch)
+    bool osnap_next = false;            // the previous level was the first pull of a lazy batch
+    bool lean_off = false;              // a lean first-row pass overflowed (see k_bu_first)
+    bool lean_ran = false;              // this level ran one (its overflow count is c.touched)
+    bool old_stale = false;             // k_td_fused levels updated only vis_[cur]
+  };
+  struct Small {
+    unsigned long long* F;
+    unsigned long long* E;
+    uint64_t* alive[2];
+    uint64_t* gmask;
+  };
+
+ private:
+  Small small() {
+    Small r;
+    r.F = small_.as<unsigned long long>();
+    r.E = r.F + 64 * 16;
+    r.alive[0] = (uint64_t*)(r.E + 64 * 16);
+    r.alive[1] = r.alive[0] + 16;
+    r.gmask = r.alive[1] + 16;
+    return r;
+  }
+  template <int W>
+  uint32_t* slabF(int row) { return slabF_.as<uint32_t>() + (size_t)row * 64 * W; }
+  template <int W>
+  unsigned long long* slabE(int row) {
+    return slabE_.as<unsigned long long>() + (size_t)row * 64 * W;
+  }
+
+  // ---- bitpar_solver.hip
+  template <int W, bool COUNT>
+  void start_batch(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids, Loop& S,
+                   hipStream_t s);
+  template <int W, bool COUNT>
+  void levels(Loop& S, RunStats* st, hipStream_t s);
+  template <int W, bool COUNT>
+  void batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids, int64_t* F,
+                  int64_t* edges2, RunStats* st, hipStream_t s);
+  void run_batch(int w, int64_t k0, int64_t nb, const int64_t* qoff, const int32_t* qids,
+                 int64_t* F, int64_t* edges2, RunStats* st, hipStream_t s);
+  // ---- bitpar_push.hip: one top-down level (returns the counter-slab rows it wrote)
+  template <int W, bool COUNT>
+  int level_td(Loop& S, hipStream_t s);
+  template <int W, bool COUNT>
+  void td_batch(Loop& S, RunStats* st, hipStream_t s);
+  // ---- bitpar_pull.hip: one bottom-up level (returns the counter-slab rows it wrote)
+  template <int W, bool COUNT>
+  int level_bu(Loop& S, hipStream_t s);
+  const int32_t* prefix_lens(int32_t H, hipStream_t s);
+  const int32_t* first_nbr(hipStream_t s);
+  int32_t code_bound(double min_deg);
+  // ---- bitpar_hybrid.hip
+  template <int W>
+  void phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,
+                    int64_t n_eff, bool count_l1, const int32_t* wbeg, uint64_t* send,
+                    int64_t* out, RunStats* st, hipStream_t s, int64_t* coded_len);
+  template <int W>
+  void phase_c_impl(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
+                    const uint64_t* recv, const int64_t* reduced, int64_t* F_out, RunStats* st,
+                    hipStream_t s);
+  template <int W>
+  void code_send(const uint64_t* vis, uint64_t* staging, int64_t cnt, int part, int nparts,
+                 const int32_t* wbeg, uint64_t* send, int64_t* coded_len, hipStream_t s);
+  // scratch of the exchange coding: bitmap words, popcounts and their inclusive scan per chunk
+  struct CodeWs {
+    uint64_t* bits;
+    int64_t* pop;
+    int64_t* incl;
+    void* tmp;
+    size_t tmp_bytes;
+  };
+  CodeWs code_ws(int64_t chunks);
+
+  // device-driven top-down batches run k_td_fused levels (needs every row of vis_[cur] valid,
+  // i.e. no lazy batch; the edge-counting pass keeps expand + finalize + k_count_frontier)
+  double alpha_eff() const {
+    return fused_batches<false>() ? std::min(opt.alpha, kAlphaLow) : opt.alpha;
+  }
+  template <bool COUNT>
+  bool fused_batches() const {
+    return !COUNT && tun_.td_fused && tun_.batch > 1 && g_.max_degree <= kSmallDeg &&
+           (double)g_.nnz <= kTdFusedDeg * (double)std::max<int64_t>(g_.n, 1);
+  }
+  // push -> pull test threshold on the frontier's degree sum for the level after `done_levels`
+  // completed ones (the vertex half of the direction test, see levels())
+  double gamma_for(uint32_t done_levels) const {
+    return done_levels == 1 && tun_.gamma2 >= 0 ? tun_.gamma2 : tun_.gamma;
+  }
+
+  // 1 + the last vertex with deg > 0 (cached per graph buffers: relabelling replaces them).
+  // Vertices beyond it are never active, never neighbours: level loops and clears skip them.
+  int64_t n_eff() {
+    if (eff_key_[0] != (const void*)g_.rowptr || eff_key_[1] != (const void*)g_.col ||
+        eff_key_[2] != (const void*)g_.old2new) {
+      n_eff_ = hybrid_extent(g_);
+      eff_key_[0] = g_.rowptr;
+      eff_key_[1] = g_.col;
+      eff_key_[2] = g_.old2new;
+    }
+    return n_eff_;
+  }
+
+  HostCtr read_ctr(hipStream_t s) {
+    MSBFS_HIP_CHECK(hipMemcpyAsync(hctr_->p, ctr_.p, sizeof(Ctr), hipMemcpyDeviceToHost, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    const Ctr* c = hctr_->as<Ctr>();
+    return HostCtr{c->act2.v, c->actw2.v, c->fl2.v, c->touched.v, c->ef2.v, c->eu2.v, c->ev2.v};
+  }
+
+  // copy the small block (F, E, alive, gmask) to pinned host memory and wait
+  const unsigned long long* read_small(hipStream_t s) {
+    MSBFS_HIP_CHECK(hipMemcpyAsync(hsmall_->p, small_.p, small_.bytes, hipMemcpyDeviceToHost, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    return hsmall_->as<unsigned long long>();
+  }
+
+  // ---- fixed policy constants (formerly environment knobs; measured, see README)
+  static constexpr double kFilterFrac = 0.5;  // filter unvisited neighbours while ev < frac*nnz
+  static constexpr int kWideLater = 1024;     // wide split after the first bottom-up level
+  static constexpr int kLeanLevel = 3;        // first pull level (1-based) that may run lean
+  static constexpr int kTdGrid = 1024;        // blocks of the device-driven batches' kernels
+  static constexpr int kTdRed = 6;            // fused levels per k_level_reduce_multi launch
+  // push -> pull threshold (Beamer's alpha) on graphs with max degree <= kSmallDeg (fused
+  // top-down levels). Road grid 4896^2, 256 groups: alpha 14 pulls from ~1.7M frontier vertices
+  // on and takes 3030 ms, alpha 4 stays top-down (1648 ms batched)
+  static constexpr double kAlphaLow = 4.0;
+  // fused levels only below this mean degree (road-like graphs): denser low-degree graphs pull
+  // after a few levels (uniform n = 16M, m = 128M, 1024 groups: 29.6 ms vs 32.3 ms fused)
+  static constexpr double kTdFusedDeg = 8.0;
+  static constexpr int kBatch = 64;  // most levels per device-driven batch
+
+  const DeviceGraph& g_;
+  Tuning tun_;
+  int maxW_ = 1;
+  DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
+      ctr_, small_, pairs_, slabF_, slabE_, anyvis_, desc_;
+  size_t scan_bytes_ = 0;
+  std::unique_ptr<PinnedBuf> hctr_, hsmall_;
+  int32_t epoch_ = 0;
+  int64_t n_eff_ = 0;
+  const void* eff_key_[3] = {nullptr, nullptr, nullptr};
+  DevBuf plen_;
+  DevBuf first_;
+  DevBuf code_ws_;
+  const void* first_key_[2] = {nullptr, nullptr};
+  bool first_ok_ = true;  // the first-neighbour array fits (RMAT-30: no room; col[rowptr[v]])
+  const void* plen_key_[2] = {nullptr, nullptr};
+  int32_t plen_h_ = 0;
+  DevBuf fbm_[2];   // frontier bitmaps of the fused levels (n bits each)
+  DevBuf asnap_;    // any-visited bitmap at the start of a lazy batch's first pull level
+  std::map<int64_t, int32_t> code_bound_;
+  const void* code_key_[2] = {nullptr, nullptr};
+  int batch_next_ = 4;  // levels of the next device-driven batch (doubles while the frontier lives)
+  DevBuf bctr_;  // (kBatch+1) Ctr slots, then (kBatch+1) x 16 alive words
+  std::unique_ptr<PinnedBuf> hbctr_;
+};
+
+// explicit instantiation of a member template for every word count (W) and counting mode
+#define MSBFS_BP_FOR_W(X) X(1) X(2) X(4) X(8) X(16)
+
+}  // namespace bp
+}  // namespace msbfs

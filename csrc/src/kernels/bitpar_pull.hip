@@ -1,0 +1,321 @@
+// Bit-parallel MS-BFS solver: bottom-up (pull) levels — active lists, sparse row codes, prefix
+// pull + tail push on the first pull level, narrow / lean / hub-chunk pulls after it
+// (level_bu). Design overview: bitpar/solver.hpp; kernels: bitpar/pull.hpp.
+#include <algorithm>
+
+#include "bitpar/init.hpp"
+#include "bitpar/pull.hpp"
+#include "bitpar/solver.hpp"
+
+namespace msbfs {
+namespace bp {
+
+// plen[v] = row prefix length with ids < H for every vertex (cached per graph buffers and H)
+const int32_t* BitparSolver::prefix_lens(int32_t H, hipStream_t s) {
+  if (plen_key_[0] != (const void*)g_.rowptr || plen_key_[1] != (const void*)g_.col ||
+      plen_h_ != H) {
+    plen_.ensure((size_t)std::max<int64_t>(g_.n, 1) * sizeof(int32_t));
+    k_prefix_lens<<<grid_for(g_.n, kBlock, 8192), kBlock, 0, s>>>(g_.rowptr, g_.col, g_.n, H,
+                                                                   plen_.as<int32_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+    plen_key_[0] = g_.rowptr;
+    plen_key_[1] = g_.col;
+    plen_h_ = H;
+  }
+  return plen_.as<int32_t>();
+}
+
+// first[v] for every vertex (cached per graph buffers like prefix_lens); nullptr when the 4n
+// bytes do not fit comfortably (RMAT-30): k_bu_first then reads col[rowptr[v]]
+const int32_t* BitparSolver::first_nbr(hipStream_t s) {
+  if (!first_ok_) return nullptr;
+  if (first_key_[0] != (const void*)g_.rowptr || first_key_[1] != (const void*)g_.col) {
+    const size_t bytes = (size_t)std::max<int64_t>(g_.n, 1) * sizeof(int32_t);
+    if (first_.bytes < bytes) {
+      size_t fr = 0, tot = 0;
+      MSBFS_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+      if (fr < bytes + ((size_t)2 << 30)) {
+        first_ok_ = false;
+        return nullptr;
+      }
+    }
+    first_.ensure(bytes);
+    k_first_nbr<<<grid_for(g_.n, kBlock, 8192), kBlock, 0, s>>>(g_.rowptr, g_.col, g_.n,
+                                                                 first_.as<int32_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+    first_key_[0] = g_.rowptr;
+    first_key_[1] = g_.col;
+  }
+  return first_.as<int32_t>();
+}
+
+// first id with degree < min_deg (rounded to a power of two, cached per graph); 0 when the
+// graph keeps the user's ids (no degree order to exploit)
+int32_t BitparSolver::code_bound(double min_deg) {
+  if (!g_.old2new) return 0;
+  if (code_key_[0] != (const void*)g_.rowptr || code_key_[1] != (const void*)g_.col) {
+    code_bound_.clear();
+    code_key_[0] = g_.rowptr;
+    code_key_[1] = g_.col;
+  }
+  int64_t d = 1;
+  while (d < (int64_t)min_deg && d < ((int64_t)1 << 40)) d <<= 1;
+  auto it = code_bound_.find(d);
+  if (it != code_bound_.end()) return it->second;
+  DevBuf b;
+  b.alloc(sizeof(int32_t));
+  k_degree_bound<<<1, 1>>>(g_.rowptr, g_.n, d, b.as<int32_t>());
+  MSBFS_HIP_CHECK(hipGetLastError());
+  int32_t h = 0;
+  MSBFS_HIP_CHECK(hipMemcpy(&h, b.p, sizeof(h), hipMemcpyDeviceToHost));
+  code_bound_[d] = h;
+  return h;
+}
+
+template <int W, bool COUNT>
+int BitparSolver::level_bu(Loop& S, hipStream_t s) {
+  using L = Lay<W>;
+  const int64_t n = g_.n;
+  const Small sm = small();
+  const int grid = kMaxGrid;
+  int rows = 0;  // slab rows written by this level's counting kernels
+  uint64_t* R = vis_[S.cur].as<uint64_t>();
+  uint64_t* O = vis_[S.cur ^ 1].as<uint64_t>();
+  const uint64_t* alive = sm.alive[S.alv];
+  if (S.old_stale) {
+    // fused top-down levels wrote only vis_[cur]; pulls write the other buffer's rows of the
+    // active vertices and read both buffers' rows of the finished ones afterwards
+    const size_t vb = (size_t)std::max<int64_t>(n_eff(), 1) * W * sizeof(uint64_t);
+    MSBFS_HIP_CHECK(hipMemcpyAsync(O, R, vb, hipMemcpyDeviceToDevice, s));
+    S.old_stale = false;
+  }
+  const int next_wide = std::max(opt.wide_degree, kWideLater);
+  if (!S.have_active) {
+    // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
+    // off only for much higher degrees, so later lists are split at a higher threshold
+    const int wide0 = S.bu_levels == 0 ? opt.wide_degree : next_wide;
+    k_build_active<4096><<<grid_for(S.cnt, 4096, INT32_MAX), kBlock, 0, s>>>(
+        S.cnt, S.part, S.nparts, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
+        actw_[0].as<int32_t>(), ctr_.as<Ctr>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+    const HostCtr c = read_ctr(s);
+    S.nact = c.act2;
+    S.nactw = c.actw2;
+    S.have_active = true;
+    MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
+  }
+  const bool first_bu = S.bu_levels == 0;
+  ++S.bu_levels;
+  if (S.fsrc_acc) {
+    // bottom-up does not read frontier bits; clear the pending top-down ones so acc_[ac]
+    // is all-zero and can collect the wide vertices' chunk results
+    k_zero_acc<W><<<grid_for(S.nf * L::G, kBlock), kBlock, 0, s>>>(
+        fl_[S.fc].as<int32_t>(), S.nf, acc_[S.ac].as<uint64_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  // lazy batch, first pull level: rows of vertices nobody visited yet may be stale, so every
+  // gathered row must be one of a visited vertex (always filter), and probes / own rows use a
+  // snapshot of the any-visited bitmap (a vertex first visited during the level may be
+  // probed before its row is written). From the next pull level on the read buffer holds
+  // this level's rows, valid for every vertex a pull can reach (see start_batch).
+  const bool lazy_first = S.lazy && first_bu;
+  const uint32_t* snap = nullptr;
+  if (lazy_first) {
+    MSBFS_HIP_CHECK(hipMemcpyAsync(asnap_.p, anyvis_.p, anyvis_.bytes, hipMemcpyDeviceToDevice, s));
+    snap = asnap_.as<uint32_t>();
+  }
+  // filtered levels probe the any-visited bitmap before gathering a neighbour's row (while
+  // fewer than kFilterFrac of the edges lead to visited vertices, and always on a lazy batch's
+  // first pull); filter_from = first id that is probed (0) or INT32_MAX (no probes)
+  const bool filter = lazy_first || (double)S.ev < kFilterFrac * (double)g_.nnz;
+  const int32_t filter_from = filter ? 0 : INT32_MAX;
+  // probes of the lowest ids (the hubs after degree relabelling) read an LDS copy of their
+  // bitmap words: 56 KB (ids < 458752, two blocks per CU) or, where one 1024-thread block per CU
+  // has the LDS to itself, 128 KB (ids < 1M)
+  constexpr int kHubW = 14336, kHubBig = 32768;
+  const bool hub_lds = filter_from == 0 && n > (int64_t)kHubW * 32 * 4;
+  const bool hub_big = n > (int64_t)kHubBig * 32 * 4;
+  // counting fused into the traversal kernels (the edge-count pass keeps k_count_frontier)
+  constexpr bool FUSE = !COUNT;
+  // prefix pull + tail push on the first bottom-up level (see k_push_tail): the pulls stop at
+  // the small hub bitmap's bound H = 458752 (RMAT-26 level 2: 16.8 ms vs 18.1 at the 1M bound)
+  constexpr int32_t kPfxH = kHubW * 32;
+  const bool pfx = tun_.pfx == 2 && first_bu && S.level == 2 && hub_lds && hub_big &&
+                   g_.rows_sorted && n <= INT32_MAX;
+  // sparse row codes for the first bottom-up level after level 1 (see k_build_codes). With
+  // the prefix pull only ids < H and the tail pushers' own codes are ever read: the codes of
+  // [code_from, H) plus those of the frontier vertices >= H (not 4 bytes for every id).
+  int32_t code_from = kNoCodes;
+  const uint32_t* codes = nullptr;
+  if (first_bu && S.level == 2 && tun_.codes && W >= 8 && S.ef0 > 0 && n <= INT32_MAX) {
+    const int64_t ne = n_eff();
+    code_from = (int32_t)std::min<int64_t>(
+        code_bound(tun_.code_deg * (double)g_.nnz / (double)S.ef0), ne);
+    if (code_from < ne) {
+      uint32_t* cb = touched_.as<uint32_t>();  // n entries
+      const int64_t hi = pfx ? std::min<int64_t>(std::max<int64_t>(kPfxH, code_from), ne) : ne;
+      const int64_t nl = pfx ? S.nf : 0;
+      k_build_codes<W><<<grid_for(hi - code_from + nl, kBlock, 8192), kBlock, 0, s>>>(
+          R, anyvis_.as<uint32_t>(), code_from, hi, fl_[S.fc].as<int32_t>(), nl, cb);
+      MSBFS_HIP_CHECK(hipGetLastError());
+      codes = cb;
+    } else {
+      code_from = kNoCodes;
+    }
+  }
+  const int32_t* plen = pfx ? prefix_lens(kPfxH, s) : nullptr;
+  if (pfx) {
+    ++epoch_;
+    k_push_tail<W><<<grid_for(S.nf * 64, kBlock, 8192), kBlock, 0, s>>>(
+        fl_[S.fc].as<int32_t>(), S.nf, kPfxH, g_.rowptr, g_.col, R, codes, code_from,
+        done_.as<uint32_t>(), S.part, S.nparts, acc_[S.ac].as<uint64_t>(),
+        stamp_.as<int32_t>(), epoch_);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  if (S.nact) {
+    if (pfx) {
+      constexpr int BT = 1024;
+      const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
+      // 4-neighbour steps: 122 VGPRs, no spills (8-neighbour steps spilled at the 128-VGPR
+      // bound): RMAT-26 5.17 -> 4.96 ms (the full pulls of level 3 keep 8: 5.8 vs 6.8 ms)
+      auto kn = FUSE ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE, true, true, 4>
+                     : k_bu_narrow<W, COUNT, BT, kHubW, false, true, true>;
+      kn<<<gn, BT, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
+                           sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
+                           fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+                           anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+                           next_wide, slabF<W>(rows), acc_[S.ac].as<uint64_t>(),
+                           stamp_.as<int32_t>(), epoch_, plen, nullptr, snap);
+      if (FUSE) rows += gn;
+    } else if (hub_lds) {
+      constexpr int BT = 1024;
+      const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
+      // the narrow kernel runs one 1024-thread block per CU anyway (VGPR-bound), so its LDS
+      // has room for a 4x larger hub bitmap
+      auto kn = hub_big ? k_bu_narrow<W, COUNT, BT, kHubBig, FUSE>
+                        : k_bu_narrow<W, COUNT, BT, kHubW, FUSE>;
+      kn<<<gn, BT, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
+                           sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
+                           fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+                           anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+                           next_wide, slabF<W>(rows), nullptr, nullptr, 0, nullptr, nullptr, snap);
+      if (FUSE) rows += gn;
+    } else {
+      const int gn = grid_for(S.nact, L::TILE, grid);
+      // FILT = false: no probe code at all (fewer VGPRs) on the levels that load every row
+      const bool filt = filter_from != INT32_MAX;
+      // short first step (one row) from the third bottom-up level on, or with few words: by
+      // then most vertices are covered by their first neighbour (RMAT-26, 1024 groups: level
+      // 4 3.1 -> 2.5 ms; level 3 prefers full steps: 6.5 vs 6.7 ms)
+      const bool short1 = S.bu_levels >= 3 || W <= 4;
+      if (tun_.lean && !S.lean_off && FUSE && !filt && S.bu_levels >= kLeanLevel &&
+          S.nact >= tun_.lean_min) {
+        S.lean_ran = true;
+        // lean first pass, then the regular pull over the vertices it could not finish
+        const int gl = grid_for(S.nact, L::TILE, grid);
+        k_bu_first<W><<<gl, kBlock, 0, s>>>(
+            act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+            done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s));
+        MSBFS_HIP_CHECK(hipGetLastError());
+        rows += gl;
+        k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
+            touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+            done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+            next_wide, slabF<W>(rows), nullptr, nullptr, 0, nullptr, &ctr_.as<Ctr>()->touched.v,
+            nullptr);
+        MSBFS_HIP_CHECK(hipGetLastError());
+        rows += gn;
+      } else {
+        auto kn = FUSE ? (filt ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, true>
+                               : short1 ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1>
+                                        : k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false>)
+                       : (filt ? k_bu_narrow<W, COUNT, kBlock, 0, false, true>
+                               : k_bu_narrow<W, COUNT, kBlock, 0, false, false>);
+        kn<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
+                                 sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
+                                 fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+                                 anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+                                 next_wide, slabF<W>(rows), nullptr, nullptr, 0, nullptr, nullptr,
+                                 snap);
+        if (FUSE) rows += gn;
+      }
+    }
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  if (S.nactw) {
+    if (pfx) {  // chunks of the row prefixes with ids < H only
+      int64_t* cnt = scan_tmp_.as<int64_t>();
+      char* t2 = (char*)scan_tmp_.p + (((size_t)S.nactw * sizeof(int64_t) + 255) & ~size_t(255));
+      const size_t tb = scan_bytes_ - (size_t)(t2 - (char*)scan_tmp_.p);
+      k_prefix_chunks<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
+          actw_[0].as<int32_t>(), S.nactw, plen, cnt);
+      MSBFS_HIP_CHECK(hipGetLastError());
+      inclusive_scan_i64(cnt, offs_.as<int64_t>(), S.nactw, t2, tb, s);
+    } else {
+      frontier_degree_scan(g_.rowptr, actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(),
+                           scan_tmp_.p, scan_bytes_, s, kChunk);
+    }
+    const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
+    // Early exit across a vertex's chunks (coop) everywhere except on an explosive first
+    // bottom-up level (level 2: hardly any row gets covered, and round-robin chunk dealing
+    // balances the hubs better). When top-down ran longer (RMAT-30: first pull at level 3,
+    // most of every hub's groups already visited) the early exit skips most chunks.
+    const int coop = !first_bu || S.level != 2 ? 1 : 0;
+    desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
+    k_chunk_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
+        actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, plen,
+        desc_.as<ChunkDesc>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+    if (hub_lds) {
+      // exact chunk count = offs[nactw - 1], read on the device (no host round trip); one
+      // block per CU with the 128-KB hub bitmap (ids < 1M) except on the prefix level, whose
+      // prefixes end at the small one's bound (two blocks per CU)
+      const bool big = hub_big && !pfx;
+      auto ck = big ? k_bu_chunks<W, 256, 1024, kHubBig> : k_bu_chunks<W, 256, 1024, kHubW>;
+      ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
+          desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
+          sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
+          coop, codes, code_from, snap);
+    } else {
+      k_bu_chunks<W, 256, kBlock, 0><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
+          desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask,
+          acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, coop, codes, code_from,
+          snap);
+    }
+    MSBFS_HIP_CHECK(hipGetLastError());
+    const int gw = grid_for(S.nactw, L::TILE, grid);
+    k_bu_wide_finalize<W, COUNT, FUSE><<<gw, kBlock, 0, s>>>(
+        actw_[0].as<int32_t>(), S.nactw, g_.rowptr, R, O, acc_[S.ac].as<uint64_t>(), alive,
+        sm.gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+        ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), act_[1].as<int32_t>(), next_wide,
+        slabF<W>(rows), snap);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    if (FUSE) rows += gw;
+  }
+  if constexpr (!FUSE) {
+    // new frontier bits = Wb & ~R (both still in place: the swap is below)
+    const int gc = grid_for(S.nact + S.nactw, L::TILE, grid);
+    k_count_frontier<W, COUNT, true><<<gc, kBlock, 0, s>>>(
+        fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(), g_.rowptr, O, R, slabF<W>(rows),
+        slabE<W>(rows));
+    MSBFS_HIP_CHECK(hipGetLastError());
+    rows += gc;
+  }
+  std::swap(act_[0], act_[1]);
+  std::swap(actw_[0], actw_[1]);
+  S.cur ^= 1;
+  S.fsrc_acc = false;
+  S.osnap_next = lazy_first;
+  return rows;
+}
+
+#define MSBFS_BP_INST(WW)                                              \
+  template int BitparSolver::level_bu<WW, false>(Loop&, hipStream_t); \
+  template int BitparSolver::level_bu<WW, true>(Loop&, hipStream_t);
+MSBFS_BP_FOR_W(MSBFS_BP_INST)
+#undef MSBFS_BP_INST
+
+}  // namespace bp
+}  // namespace msbfs

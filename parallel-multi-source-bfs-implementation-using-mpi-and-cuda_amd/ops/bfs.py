@@ -37,7 +37,10 @@ class Solver:
 
     def __init__(self, graph: DeviceGraph, algo: str = "auto", max_groups: int = 1024,
                  alpha: float = 0.0, beta: float = 0.0, wide_degree: int = 0,
-                 force_dir: int = 0, max_words: int = 0):
+                 force_dir: int = 0, max_words: int = 0, tuning=None):
+        """tuning: algorithm tuning keys of the bit-parallel solver, a dict {"gamma2": 0.5, ...}
+        or a "key=value,..." string (see msbfs_solver_tune in csrc/include/msbfs/msbfs.h);
+        unknown keys raise MsbfsError."""
         if algo not in native.ALGOS or algo == "cpu":
             raise ValueError(f"unknown device algorithm {algo!r}")
         self.graph = graph
@@ -49,6 +52,13 @@ class Solver:
         if alpha or beta or wide_degree or force_dir or max_words:
             o = native.Options(alpha, beta, wide_degree, force_dir, max_words)
             native.check(native.lib().msbfs_solver_set_options(self._h, C.byref(o)))
+        if tuning:
+            self.tune(tuning)
+
+    def tune(self, tuning) -> None:
+        spec = tuning if isinstance(tuning, str) else ",".join(
+            f"{k}={v}" for k, v in dict(tuning).items())
+        native.check(native.lib().msbfs_solver_tune(self._h, spec.encode()))
 
     def run(self, queries: QuerySet, count_edges: bool = False, stream: Optional[int] = None
             ) -> BfsResult:

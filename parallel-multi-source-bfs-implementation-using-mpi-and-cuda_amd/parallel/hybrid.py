@@ -16,7 +16,7 @@ keeps the replica but changes the split:
            block (1/N of the words); plus one small SUM all-reduce of the phase-A partial sums,
            "still alive" flags and frontier sizes. About half of those words are zero after
            level 2 (RMAT-26, 1024 groups, 8 ranks: 50.5 %): optionally (coded=True, bench
-           candidate "hybrid-coded", MSBFS_HYB_CODED=1) each destination's share travels
+           candidate "hybrid-coded", CLI --dist hybrid-coded) each destination's share travels
            zero-word coded (encode_np: a bitmap word per 64 words + the nonzero words; the
            same all-reduce carries the N x N matrix of coded lengths) and the receiver expands
            it on the GPU (Solver.hybrid_decode); see coding_default for when that pays.
@@ -77,11 +77,13 @@ def coded_bound(words: int) -> int:
 
 
 def coding_default() -> bool:
-    """Zero-word coded exchange only with MSBFS_HYB_CODED=1. Measured (RMAT-26, 1024 groups, 8
+    """Dense exchange by default (coded only when asked for: HybridRunner(coded=True), bench.py
+    candidate "hybrid-coded", CLI --dist hybrid-coded; never from a per-rank environment
+    variable, since every rank must size and call the same collectives). Measured (RMAT-26, 1024 groups, 8
     ranks emulated on one MI355X): 296 instead of 501 MB per GPU, but +0.8 ms of coding in phase
     A and +0.43 ms of decoding before phase C, so it pays only when the all-to-all runs below
     ~170 GB/s per GPU. bench.py measures it as a separate candidate ("hybrid-coded")."""
-    return os.environ.get("MSBFS_HYB_CODED", "0") == "1"
+    return False
 
 
 def encode_np(words: np.ndarray) -> np.ndarray:

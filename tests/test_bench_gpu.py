@@ -83,8 +83,8 @@ def test_bench_multi_rank_gloo_shared_gpu(ranks, dist):
     buffers, and bench.py checks each decomposition's F against the round-robin pass."""
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", str(ranks), "--master-addr", "127.0.0.1",
-                        "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--scale",
-                        "16", "--groups", "200", "--steps", "2", "--warmup", "1", "--dist", dist,
+                        "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus",
+                        str(ranks), "--scale", "16", "--groups", "200", "--steps", "2", "--warmup", "1", "--dist", dist,
                         "--backend", "gloo", "--verify", "4"],
                        capture_output=True, text=True, timeout=110, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -94,3 +94,30 @@ def test_bench_multi_rank_gloo_shared_gpu(ranks, dist):
         assert js["config"]["parallelism"].startswith(f"hybrid{ranks}")
     else:
         assert set(js["config"]["candidates_ms"]) == {"roundrobin", "hybrid", "hybrid-coded"}
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts the two ranks itself (the driver's
+    plain `python3 bench.py --gpus N` must measure N ranks, not one): n_gpus 2 in the JSON line,
+    the timed F equal to the untimed pass, groups checked against the distance solver."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--backend", "gloo", "--scale", "16", "--groups", "200", "--steps", "2",
+                        "--warmup", "1", "--verify", "8"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert js["n_gpus"] == 2 and js["value"] > 0
+    assert js["verified"] == 8 and js["config"]["timed_F_equals_untimed"]
+
+
+def test_bench_one_gpu_self_verifies():
+    """The default headline run checks itself: verified >= 8 groups against the distance solver
+    (untimed) and the last timed step's F equal to the untimed pass."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--scale", "18",
+                        "--groups", "256", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert js["verified"] >= 8 and js["n_gpus"] == 1

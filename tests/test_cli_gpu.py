@@ -128,13 +128,13 @@ def test_python_cli_gpu(tmp_path, msbfs_pkg, extra):
 @pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
 @pytest.mark.parametrize("ranks,K,comm", [(3, 300, "mpi"), (2, 130, "mpi"), (1, 200, "rccl")])
 def test_cli_gpu_hybrid_coded_exchange(tmp_path, msbfs_pkg, ranks, K, comm):
-    """MSBFS_HYB_CODED=1: the hybrid all-to-all carries zero-word coded segments (sizes from the
+    """--dist hybrid-coded: the hybrid all-to-all carries zero-word coded segments (sizes from the
     coded-length matrix in the phase-A all-reduce) and every rank decodes them on the GPU; the
     report and F vector must equal the CPU oracle's (host MPI staging and a real RCCL group)."""
     m = msbfs_pkg
     g, qs, gp, qp = _files(tmp_path, m, K, 4)
     ref = m.cpu_bfs(g, qs, count_edges=True)
     r = _run([MPIEXEC, "-n", str(ranks), _cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo",
-              "bitpar", "--dist", "hybrid", "--comm", comm, "--json"], {"MSBFS_HYB_CODED": "1"})
+              "bitpar", "--dist", "hybrid-coded", "--comm", comm, "--json"])
     js = _check(r, ref, m, ranks)
     assert js["comm"] == comm

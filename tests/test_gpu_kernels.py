@@ -207,7 +207,7 @@ def test_bitpar_level_trace(msbfs_pkg):
 
 
 @pytest.mark.parametrize("K", [300, 1024])
-def test_bitpar_sparse_codes_relabelled(msbfs_pkg, K, monkeypatch):
+def test_bitpar_sparse_codes_relabelled(msbfs_pkg, K):
     """First bottom-up level with sparse single-group row codes (k_build_codes) on a degree-
     relabelled device RMAT graph: identical F with the codes on, off, and against the CPU oracle."""
     m = msbfs_pkg
@@ -217,16 +217,15 @@ def test_bitpar_sparse_codes_relabelled(msbfs_pkg, K, monkeypatch):
     g.relabel_by_degree()
     out = {}
     for codes in ("1", "0"):
-        monkeypatch.setenv("MSBFS_CODES", codes)
-        monkeypatch.setenv("MSBFS_CODE_DEG", "0.5")  # codes for most ids, dense fallback exercised
-        with m.Solver(g, "bitpar", max_groups=K) as s:
+        # code_deg 0.5: codes for most ids, the dense fallback exercised
+        with m.Solver(g, "bitpar", max_groups=K, tuning={"codes": codes, "code_deg": 0.5}) as s:
             out[codes] = s.run(qs).F
     assert np.array_equal(out["1"], ref.F)
     assert np.array_equal(out["0"], ref.F)
     g.close()
 
 
-def test_bitpar_prefix_pull_tail_push(msbfs_pkg, monkeypatch):
+def test_bitpar_prefix_pull_tail_push(msbfs_pkg):
     """First bottom-up level as prefix pull (ids below the LDS hub bound) + tail push (k_push_tail)
     on a relabelled RMAT-23 (n = 8M, large enough for the 128-KB hub bitmap): identical F with
     the prefix mode on and off, and equal to the per-group distance solver on a sample."""
@@ -235,30 +234,27 @@ def test_bitpar_prefix_pull_tail_push(msbfs_pkg, monkeypatch):
     g.relabel_by_degree()
     qs = m.QuerySet.random(g.n, 1024, 16, seed=11)
     out = {}
-    for pfx in ("2", "1", "0"):  # prefix bound 458752 / 1M / off
-        monkeypatch.setenv("MSBFS_PFX", pfx)
-        with m.Solver(g, "bitpar", max_groups=qs.K) as s:
+    for pfx in ("2", "0"):  # prefix bound 458752 / off (whole rows)
+        with m.Solver(g, "bitpar", max_groups=qs.K, tuning={"pfx": pfx}) as s:
             out[pfx] = s.run(qs).F
             tr = s.level_trace()
         assert tr[0]["dir"] == "T" and tr[1]["dir"] == "B"  # the prefix level is level 2
-    assert np.array_equal(out["1"], out["0"]) and np.array_equal(out["2"], out["0"])
+    assert np.array_equal(out["2"], out["0"])
     sub = qs.subset(np.arange(0, 1024, 128))
     with m.Solver(g, "dist") as ds:
-        assert np.array_equal(ds.run(sub).F, out["1"][::128])
+        assert np.array_equal(ds.run(sub).F, out["2"][::128])
     g.close()
 
 
 @pytest.mark.parametrize("dirs", ["", "TBBBBBBBBBBBBBBBBBBB", "TBBTBBTBBTBBTBBT", "TBTBTBTBTBTBTBTB",
                                   "TTBBTTBBTTBB"])
-def test_bitpar_forced_direction_plans(msbfs_pkg, monkeypatch, dirs):
-    """Forced per-level direction plans (MSBFS_DIRS): push levels right after pull levels read
+def test_bitpar_forced_direction_plans(msbfs_pkg, dirs):
+    """Forced per-level direction plans (tuning dirs): push levels right after pull levels read
     the frontier as the difference of the two visited buffers, pulls after pushes start from the
     top-down accumulator. Runs without the edge count (the fused-count kernels) on a relabelled
     RMAT, uniform and road-like graphs, several batches (K > 64 * W) included, and reuses the
     solver (stale rows of the previous run must not leak)."""
     m = msbfs_pkg
-    if dirs:
-        monkeypatch.setenv("MSBFS_DIRS", dirs)
     dg = m.DeviceGraph.rmat(14, 16, 5, device=0)
     hg = dg.download()  # original ids (after relabelling download() gives internal ones)
     dg.relabel_by_degree()
@@ -268,22 +264,21 @@ def test_bitpar_forced_direction_plans(msbfs_pkg, monkeypatch, dirs):
     for dev, host, K in cases:
         qs = m.QuerySet.random(host.n, K, 4, seed=K)
         ref = m.cpu_bfs(host, qs)
-        with m.Solver(dev, "bitpar", max_groups=min(K, 1024)) as s:
+        with m.Solver(dev, "bitpar", max_groups=min(K, 1024),
+                      tuning={"dirs": dirs} if dirs else None) as s:
             r = s.run(qs)
             r2 = s.run(qs)
         assert np.array_equal(r.F, ref.F), (dirs, K)
         assert np.array_equal(r2.F, ref.F), (dirs, K)
 
 
-@pytest.mark.parametrize("knobs", [{"MSBFS_LEAN_MIN": "0"}, {"MSBFS_LEAN": "0"},
-                                   {"MSBFS_LAZY": "0"}, {"MSBFS_LAZY": "0", "MSBFS_LEAN_MIN": "0"}])
-def test_bitpar_lean_and_lazy_paths(msbfs_pkg, monkeypatch, knobs):
+@pytest.mark.parametrize("knobs", [{"lean_min": 0}, {"lean": 0}, {"lazy": 0},
+                                   {"lazy": 0, "lean_min": 0}])
+def test_bitpar_lean_and_lazy_paths(msbfs_pkg, knobs):
     """The lean first-row pass on late pull levels (k_bu_first + overflow pull; forced on small
-    lists with MSBFS_LEAN_MIN=0) and the lazy batches without the visited-buffer fill agree with
+    lists with tuning lean_min=0) and the lazy batches without the visited-buffer fill agree with
     the CPU oracle, with each switched on and off, over several batches and a reused solver."""
     m = msbfs_pkg
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
     dg = m.DeviceGraph.rmat(15, 16, 7, device=0)
     hg = dg.download()
     dg.relabel_by_degree()
@@ -293,7 +288,7 @@ def test_bitpar_lean_and_lazy_paths(msbfs_pkg, monkeypatch, knobs):
     for dev, host, K in cases:
         qs = m.QuerySet.random(host.n, K, 8, seed=K + 1)
         ref = m.cpu_bfs(host, qs)
-        with m.Solver(dev, "bitpar", max_groups=min(K, 1024)) as s:
+        with m.Solver(dev, "bitpar", max_groups=min(K, 1024), tuning=knobs) as s:
             r = s.run(qs)
             r2 = s.run(qs)
         assert np.array_equal(r.F, ref.F), (knobs, K)
@@ -350,7 +345,7 @@ def test_device_algos_property(msbfs_pkg):
 
 
 @pytest.mark.parametrize("fused", ["1", "0", "bitmap"])
-def test_bitpar_fused_topdown_batches(msbfs_pkg, monkeypatch, fused):
+def test_bitpar_fused_topdown_batches(msbfs_pkg, fused):
     """Low-degree graphs run device-driven top-down batches; by default each level is one
     k_td_fused kernel (claims bits with atomicOr on the visited row, keeps only vis[cur] current).
     Road-like grids stay top-down; the uniform graphs switch to pulls after fused levels (a level
@@ -358,10 +353,9 @@ def test_bitpar_fused_topdown_batches(msbfs_pkg, monkeypatch, fused):
     first); repeated runs reuse the buffers; W = 1, 4, 16.
     "bitmap": the list/bitmap choice forced to the bitmap walk, short batches."""
     m = msbfs_pkg
-    monkeypatch.setenv("MSBFS_TD_FUSED", "0" if fused == "0" else "1")
+    tun = {"td_fused": 0 if fused == "0" else 1}
     if fused == "bitmap":  # every level after a batch's first walks the frontier bitmap
-        monkeypatch.setenv("MSBFS_TD_BM", "1")
-        monkeypatch.setenv("MSBFS_BATCH", "5")
+        tun.update(td_bm=1, batch=5)
     graphs = [m.Graph.grid(90, 110, 0.65, 0, 3), m.Graph.grid(50, 50, 0.9, 20, 4),
               m.Graph.uniform(20000, 160000, 5), m.Graph.uniform(6000, 3500, 6),
               m.Graph.uniform(60000, 240000, 7)]
@@ -370,13 +364,13 @@ def test_bitpar_fused_topdown_batches(msbfs_pkg, monkeypatch, fused):
         for K in (1, 64, 200, 1024):
             qs = m.QuerySet.random(g.n, K, 3, seed=K + gi)
             ref = m.cpu_bfs(g, qs)
-            with m.Solver(dg, "bitpar", max_groups=K) as s:
+            with m.Solver(dg, "bitpar", max_groups=K, tuning=tun) as s:
                 for _ in range(2):
                     r = s.run(qs)
                     assert np.array_equal(r.F, ref.F), (gi, K, fused)
 
 
-def test_bitpar_fused_level_records_match(msbfs_pkg, monkeypatch):
+def test_bitpar_fused_level_records_match(msbfs_pkg):
     """The fused levels take the frontier's degree sum from the next level's row offsets (and
     at a batch's last level from the appends): per-level frontier sizes and degree sums — the
     direction heuristic's inputs — equal the expand + finalize path's (push levels only: the
@@ -388,9 +382,8 @@ def test_bitpar_fused_level_records_match(msbfs_pkg, monkeypatch):
         qs = m.QuerySet.random(g.n, K, 4, seed=K)
         recs = {}
         for fused in ("1", "0"):
-            monkeypatch.setenv("MSBFS_TD_FUSED", fused)
-            monkeypatch.setenv("MSBFS_BATCH", "7")
-            with m.Solver(dg, "bitpar", max_groups=K, force_dir=1) as s:
+            with m.Solver(dg, "bitpar", max_groups=K, force_dir=1,
+                          tuning={"td_fused": fused, "batch": 7}) as s:
                 s.run(qs)
                 recs[fused] = [(r["level"], r["dir"], r["nf"], r["ef"], r["nf_next"])
                                for r in s.level_trace()]
@@ -398,13 +391,12 @@ def test_bitpar_fused_level_records_match(msbfs_pkg, monkeypatch):
 
 
 @pytest.mark.parametrize("gamma2,want", [("0", "B"), ("100", "T")])
-def test_bitpar_level2_direction_threshold(msbfs_pkg, monkeypatch, gamma2, want):
-    """MSBFS_GAMMA2 decides level 2's direction for few groups: a pull with the prefix pull + tail
+def test_bitpar_level2_direction_threshold(msbfs_pkg, gamma2, want):
+    """Tuning gamma2 decides level 2's direction for few groups: a pull with the prefix pull + tail
     push (0) or a push that makes level 3 the first, whole-row pull (100). Both plans must give
     the oracle's F; the level records show which one ran."""
     m = msbfs_pkg
-    monkeypatch.setenv("MSBFS_GAMMA2", gamma2)
-    monkeypatch.setenv("MSBFS_GAMMA", "100")  # the later levels' vertex test out of the way
+    tun = {"gamma2": gamma2, "gamma": 100}  # (gamma 100: the later levels' vertex test out of the way)
     dg = m.DeviceGraph.rmat(16, 16, 9, device=0)
     hg = dg.download()
     dg.relabel_by_degree()
@@ -412,8 +404,48 @@ def test_bitpar_level2_direction_threshold(msbfs_pkg, monkeypatch, gamma2, want)
         qs = m.QuerySet.random(hg.n, K, 16, seed=K)
         ref = m.cpu_bfs(hg, qs)
         # a tiny alpha turns Beamer's edge test off: only the vertex test decides
-        with m.Solver(dg, "bitpar", max_groups=K, alpha=1e-9) as s:
+        with m.Solver(dg, "bitpar", max_groups=K, alpha=1e-9, tuning=tun) as s:
             r = s.run(qs)
             dirs = "".join(t["dir"] for t in s.level_trace())
         assert np.array_equal(r.F, ref.F), (gamma2, K, dirs)
         assert dirs[:2] == "T" + want, (gamma2, K, dirs)
+
+
+@pytest.mark.parametrize("gamma2,want", [("0", "B"), ("100", "T")])
+@pytest.mark.parametrize("fused", [0, 1])
+def test_bitpar_level2_threshold_in_device_batches(msbfs_pkg, gamma2, fused, want):
+    """On a low-degree graph (max degree <= 64) levels 1-2 run inside a device-driven top-down
+    batch, which stops itself where the host would pull: the stop must use gamma2 for level 2
+    exactly like the host loop (0: level 2 pulls; 100: it pushes), with and without the fused
+    one-kernel levels. F must equal the oracle's either way."""
+    m = msbfs_pkg
+    g = m.Graph.uniform(30000, 240000, 8)  # mean degree 16 > 8: the batches run expand+finalize
+    g2 = m.Graph.uniform(60000, 200000, 9)  # mean degree 6.7: fused levels
+    for host in (g, g2):
+        assert int(np.diff(host.rowptr).max()) <= 64
+        dg = host.to_device(0)
+        qs = m.QuerySet.random(host.n, 64, 8, seed=3)
+        ref = m.cpu_bfs(host, qs)
+        with m.Solver(dg, "bitpar", max_groups=64, alpha=1e-9,
+                      tuning={"gamma2": gamma2, "gamma": 100, "td_fused": fused}) as s:
+            r = s.run(qs)
+            dirs = "".join(t["dir"] for t in s.level_trace())
+        assert np.array_equal(r.F, ref.F), (gamma2, dirs)
+        assert dirs[:2] == "T" + want, (gamma2, fused, dirs)
+        dg.close()
+
+
+def test_bitpar_tuning_rejects_unknown_keys(msbfs_pkg):
+    """Tuning is explicit and validated: an unknown key or a malformed value is an error, never a
+    silently ignored setting (and the distance solver accepts no keys at all)."""
+    m = msbfs_pkg
+    g = m.Graph.grid(20, 20, 1.0, 0, 1).to_device(0)
+    with m.Solver(g, "bitpar", max_groups=64) as s:
+        for bad in ("gamma3=1", "gamma2", "pfx=1", "batch=0", "dirs=TX", "lean=x"):
+            with pytest.raises(m.native.MsbfsError):
+                s.tune(bad)
+        s.tune("gamma2=0.5,lean=0,dirs=TB")
+    with m.Solver(g, "dist") as s:
+        with pytest.raises(m.native.MsbfsError):
+            s.tune("gamma=1")
+    g.close()

@@ -258,10 +258,12 @@ def test_hybrid_matches_cpu_other_graphs(msbfs_pkg, world):
 
 
 @pytest.mark.gpu
-def test_hybrid_lazy_reset_with_stale_rows(msbfs_pkg, monkeypatch):
+def test_hybrid_lazy_reset_with_stale_rows(msbfs_pkg):
     """Phase A skips the visited-buffer fill (k_zero_part_rows + the top-down anyvis guard): run
     it over buffers full of another query set's rows (a normal run, then other phases) and check
-    every result against the filled variant (MSBFS_LAZY=0) and the standard solver."""
+    every result against the filled variant (tuning lazy=0) and the standard solver; the coded
+    exchange stages its dense segments in the other visited buffer, which the next runs must not
+    depend on."""
     m = msbfs_pkg
     H = _H()
     dg = m.DeviceGraph.rmat(15, 16, 11, device=0, relabel=True)
@@ -272,9 +274,10 @@ def test_hybrid_lazy_reset_with_stale_rows(msbfs_pkg, monkeypatch):
         for world in (8, 3, 8):
             assert np.array_equal(H.emulate_ranks(s, qa, world), ref_a), world
             assert np.array_equal(H.emulate_ranks(s, qb, world), ref_b), world
+            assert np.array_equal(H.emulate_ranks(s, qa, world, coded=True), ref_a), world
         assert np.array_equal(s.run(qa).F, ref_a)
-    monkeypatch.setenv("MSBFS_LAZY", "0")
-    with m.Solver(dg, "bitpar", max_groups=1024) as s:
+        assert np.array_equal(s.run(qb).F, ref_b)
+    with m.Solver(dg, "bitpar", max_groups=1024, tuning={"lazy": 0}) as s:
         assert np.array_equal(H.emulate_ranks(s, qb, 4), ref_b)
 
 

@@ -4,7 +4,7 @@
 Runs every rank's phase A (levels 1-2, own residue class of vertices) and phase C (own groups, levels >= 3)
 sequentially on one GPU (parallel/hybrid.py emulate_ranks), checks F against the single-GPU
 solver, and prints per-rank device times plus the all-to-all volume. The estimated N-GPU step
-is max_r(A_r) + exchange + max_r(C_r); the exchange (dense; zero-word coded with MSBFS_HYB_CODED=1) is priced at
+is max_r(A_r) + exchange + max_r(C_r); the exchange (dense; zero-word coded with --coded) is priced at
 --a2a-gbps per GPU (max of send and receive side), an assumption to be replaced by the driver's measured 8-GPU runs. For comparison it also
 times round-robin (each rank runs ceil(K/N) groups on the whole graph).
 
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--no-roundrobin", action="store_true")
     ap.add_argument("--a2a-gbps", type=float, default=300.0,
                     help="assumed per-GPU all-to-all bandwidth (GB/s, max of send and receive)")
+    ap.add_argument("--coded", action="store_true", help="zero-word coded exchange")
     args = ap.parse_args()
 
     import msbfs
@@ -47,9 +48,9 @@ def main():
         print(json.dumps({"ranks": 1, "ms": round(one, 3), "device_ms": ref.stats["device_ms"]}),
               flush=True)
         for N in args.ranks:
-            H.emulate_ranks(s, qs, N)  # warm
+            H.emulate_ranks(s, qs, N, coded=args.coded)  # warm
             tim = []
-            F = H.emulate_ranks(s, qs, N, timings=tim)
+            F = H.emulate_ranks(s, qs, N, timings=tim, coded=args.coded)
             ok = bool(np.array_equal(F, ref.F))
             a = max(x["phase_a_ms"] for x in tim)
             c = max(x["phase_c_ms"] + x.get("decode_ms", 0.0) for x in tim)  # decode: receiver
@@ -63,7 +64,7 @@ def main():
                 "ranks": N, "correct": ok, "phase_a_ms_max": round(a, 3),
                 "phase_c_ms_max": round(c, 3), "a2a_MB_max": round(rb / 2**20, 1),
                 "a2a_dense_MB_max": round(max(x["dense_send_bytes"] for x in tim) / 2**20, 1),
-                "coded": H.coding_default(),
+                "coded": args.coded,
                 "a2a_ms_est": round(x_ms, 3), "hybrid_est_ms": round(a + x_ms + c, 3),
                 "roundrobin_ms_max": round(max(rr), 3),
                 "per_rank": [{k: (round(v, 3) if isinstance(v, float) else v)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel register / spill / occupancy table of a HIP source (hipcc -Rpass-analysis).
 
-    python tools/kregs.py csrc/src/kernels/bitpar.hip [name-regex]
+    python tools/kregs.py csrc/src/kernels/bitpar_pull.hip [name-regex]
 """
 import re
 import subprocess
