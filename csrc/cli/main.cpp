@@ -12,12 +12,15 @@
 //   --tune key=value,...   bit-parallel solver tuning (see msbfs_solver_tune in msbfs.h)
 //   --threads N (cpu algo)  --cache (CSR sidecar, off by default like the reference's re-read;
 //   --no-cache is accepted)  --json  --sort-rows  --no-relabel  --repeat R
+//   --spmd N   (N >= 1) single-process multi-GPU: N ranks as N threads of this process (thread r on device
+//              r % -gn), RCCL communicators from ncclCommInitAll when every rank owns a GPU
 //   --dist {auto,roundrobin,hybrid,hybrid-coded}  multi-rank decomposition (auto: hybrid when > 1
 //          rank, the bit-parallel solver and K <= one pass; see kernels/bitpar "hybrid";
 //          hybrid-coded: the same with the zero-word coded all-to-all)
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -25,6 +28,7 @@
 #include <iostream>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "comm.hpp"
@@ -41,6 +45,7 @@ struct Args {
   int numGPU = 1;
   int threads = 0;
   int repeat = 1;
+  int spmd = 0;
   bool cache = false, json = false, sort_rows = false, relabel = true;
 };
 
@@ -66,8 +71,9 @@ void maybe_inject(const char* where, int rank) {
   fail(std::string("injected fault: ") + where + " on rank " + std::to_string(rank));
 }
 
-// the communicator a failure must abort (world until the RCCL upgrade, then the upgraded one)
-Comm* g_active = nullptr;
+// the communicator a failure must abort (world until the RCCL upgrade, then the upgraded one);
+// per thread in single-process mode
+thread_local Comm* g_active = nullptr;
 
 int algo_id(const std::string& a) {
   if (a == "auto") return 0;
@@ -81,40 +87,12 @@ int algo_id(const std::string& a) {
 
 }  // namespace
 
-int main(int argc, char* argv[]) {
-  auto world = make_world_comm(&argc, &argv);
+// one rank of the job: the reference's main() body from device binding on (main.cu:226-421).
+// `world` is this rank's communicator; `upgraded`: it already is the final one (single-process
+// mode made the RCCL communicators up front with ncclCommInitAll).
+int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
   const int world_rank = world->rank();
   g_active = world.get();
-
-  if (argc < 5) {  // main.cu:204-212
-    if (world_rank == 0)
-      std::cerr << "Usage: mpirun -np <ranks> " << argv[0]
-                << " -g <graph.bin> -q <query.bin> -gn <numGPU>" << std::endl;
-    finalize_world();
-    return -1;
-  }
-
-  Args a;
-  for (int i = 1; i < argc; i++) {  // exact strcmp flags, unknown tokens ignored (main.cu:216-224)
-    const bool has = i + 1 < argc;
-    if (!strcmp(argv[i], "-g") && has) a.graph = argv[++i];
-    else if (!strcmp(argv[i], "-q") && has) a.query = argv[++i];
-    else if (!strcmp(argv[i], "-gn") && has) a.numGPU = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--algo") && has) a.algo = argv[++i];
-    else if (!strcmp(argv[i], "--comm") && has) a.comm = argv[++i];
-    else if (!strcmp(argv[i], "--dist") && has) a.dist = argv[++i];
-    else if (!strcmp(argv[i], "--gen") && has) a.gen = argv[++i];
-    else if (!strcmp(argv[i], "--qgen") && has) a.qgen = argv[++i];
-    else if (!strcmp(argv[i], "--tune") && has) a.tune = argv[++i];
-    else if (!strcmp(argv[i], "--threads") && has) a.threads = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--repeat") && has) a.repeat = std::max(1, atoi(argv[++i]));
-    else if (!strcmp(argv[i], "--cache")) a.cache = true;
-    else if (!strcmp(argv[i], "--no-cache")) a.cache = false;
-    else if (!strcmp(argv[i], "--json")) a.json = true;
-    else if (!strcmp(argv[i], "--sort-rows")) a.sort_rows = true;
-    else if (!strcmp(argv[i], "--no-relabel")) a.relabel = false;
-  }
-
   std::unique_ptr<Comm> comm;  // outlives the try block: the catch may have to abort it
   try {
     if (a.numGPU <= 0) fail("-gn must be >= 1 (the reference divides by it, main.cu:227)");
@@ -134,7 +112,7 @@ int main(int argc, char* argv[]) {
       }
       MSBFS_HIP_CHECK(hipSetDevice(device));
     }
-    comm = cpu ? std::move(world) : maybe_upgrade_rccl(std::move(world), a.comm, device);
+    comm = (cpu || upgraded) ? std::move(world) : maybe_upgrade_rccl(std::move(world), a.comm, device);
     g_active = comm.get();
 
     const auto t_pre0 = clk::now();  // main.cu:235
@@ -379,6 +357,30 @@ int main(int argc, char* argv[]) {
       std::vector<int64_t> Ft(nlocal);
       solver->run(nlocal, local.off.data(), local.ids.data(), Ft.data(), E2.data(), nullptr, stream);
     }
+    // Round robin runs its groups in passes of the solver's width (64*W groups); each pass's
+    // packed key goes into an asynchronous MIN all-reduce on the communicator's own stream
+    // while the next pass computes, so only the last pass's 8-byte reduction is exposed. Every
+    // rank issues the same number of reductions (ranks with fewer passes send NONE).
+    const int64_t pass = (cpu || hybrid || !solver) ? std::max<int64_t>(nlocal, 1)
+                                                    : std::max<int64_t>(1, solver->pass_groups());
+    const int npass_local = nlocal ? (int)(1 + (nlocal - 1) / pass) : 0;
+    const int npass = hybrid ? 1 : (int)comm->allreduce_max_f64((double)npass_local);
+    if (npass > Comm::kAsyncSlots) fail("too many solver passes for the asynchronous reduction");
+    comm->reserve_device_scratch((size_t)std::max<int64_t>(hout.size(), a.json ? K : 0) * 8);
+    int qbits = 1;
+    while ((int64_t(1) << qbits) <= K) ++qbits;
+    const uint64_t NONE = ~0ull;
+    // packed key of F[i0, i1): 1 + (F << qbits | q), NONE for no groups, 0 when F does not fit
+    auto pack = [&](int64_t i0, int64_t i1) -> uint64_t {
+      int64_t maxF = 0;
+      for (int64_t i = i0; i < i1; ++i) maxF = std::max(maxF, F[i]);
+      if (qbits >= 63 || (maxF >> (63 - qbits)) != 0) return 0;
+      uint64_t key = NONE;
+      for (int64_t i = i0; i < i1; ++i)
+        key = std::min(key, 1 + (((uint64_t)F[i] << qbits) | (uint64_t)local_to_global[i]));
+      return key;
+    };
+    std::vector<uint64_t> keys(std::max(npass, 1));
     for (int rep = 0; rep < a.repeat; ++rep) {
       comm->barrier();
       trace::Range range_compute("computation");
@@ -421,27 +423,28 @@ int main(int argc, char* argv[]) {
         solver->hybrid_phase_c(K, wbeg[me], nw_me, P, n_eff, hrecv.as<uint64_t>(), hout.data(),
                                hF.data(), &rs, stream);
         for (int64_t i = 0; i < nlocal; ++i) F[i] = hout[local_to_global[i]] + hF[i];
-      } else if (nlocal) {
-        rs = RunStats();
-        solver->run(nlocal, local.off.data(), local.ids.data(), F.data(), a.json ? E2.data() : nullptr,
-                    &rs, stream);
       }
-      maybe_inject("compute", comm->rank());
-      // ONE packed min-reduce of 1 + (F << qbits | q) keeps the lowest-index tie-break
+      // ONE packed min-reduce of 1 + (F << qbits | q) per pass keeps the lowest-index tie-break
       // (main.cu:391-396); a rank whose F would not fit next to the query index sends 0, so
       // every rank sees 0 and takes the two-pass fallback together
-      int qbits = 1;
-      while ((int64_t(1) << qbits) <= K) ++qbits;
-      int64_t maxF = 0;
-      for (int64_t f : F) maxF = std::max(maxF, f);
-      const uint64_t NONE = ~0ull;
-      uint64_t key = 0;
-      if (qbits < 63 && (maxF >> (63 - qbits)) == 0) {
-        key = NONE;
-        for (int64_t i = 0; i < nlocal; ++i)
-          key = std::min(key, 1 + (((uint64_t)F[i] << qbits) | (uint64_t)local_to_global[i]));
+      if (!cpu && !hybrid) {
+        rs = RunStats();
+        for (int b = 0; b < npass; ++b) {
+          const int64_t i0 = std::min<int64_t>((int64_t)b * pass, nlocal);
+          const int64_t i1 = std::min<int64_t>(i0 + pass, nlocal);
+          if (i1 > i0)
+            solver->run(i1 - i0, local.off.data() + i0, local.ids.data(), F.data() + i0,
+                        a.json ? E2.data() + i0 : nullptr, &rs, stream);
+          if (b + 1 == npass) maybe_inject("compute", comm->rank());
+          comm->allreduce_min_u64_async(pack(i0, i1), b);
+        }
+      } else {
+        maybe_inject("compute", comm->rank());
+        comm->allreduce_min_u64_async(pack(0, nlocal), 0);
       }
-      key = comm->allreduce_min_u64(key);
+      comm->wait_async(keys.data(), npass);
+      uint64_t key = NONE;
+      for (int b = 0; b < npass; ++b) key = std::min(key, keys[b]);
       if (key == NONE) { minF = -1; minK = -1; }
       else if (key != 0) {
         --key;
@@ -509,9 +512,70 @@ int main(int argc, char* argv[]) {
     // peers may be blocked in a collective: abort the job rather than finalize (MPI_Finalize
     // would wait for them forever)
     if (g_active && g_active->size() > 1) g_active->abort(EXIT_FAILURE);
-    finalize_world();
     return EXIT_FAILURE;
   }
-  finalize_world();
   return 0;
+}
+
+int main(int argc, char* argv[]) {
+  auto world = make_world_comm(&argc, &argv);
+  if (argc < 5) {  // main.cu:204-212
+    if (world->rank() == 0)
+      std::cerr << "Usage: mpirun -np <ranks> " << argv[0]
+                << " -g <graph.bin> -q <query.bin> -gn <numGPU>" << std::endl;
+    finalize_world();
+    return -1;
+  }
+  Args a;
+  for (int i = 1; i < argc; i++) {  // exact strcmp flags, unknown tokens ignored (main.cu:216-224)
+    const bool has = i + 1 < argc;
+    if (!strcmp(argv[i], "-g") && has) a.graph = argv[++i];
+    else if (!strcmp(argv[i], "-q") && has) a.query = argv[++i];
+    else if (!strcmp(argv[i], "-gn") && has) a.numGPU = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--algo") && has) a.algo = argv[++i];
+    else if (!strcmp(argv[i], "--comm") && has) a.comm = argv[++i];
+    else if (!strcmp(argv[i], "--dist") && has) a.dist = argv[++i];
+    else if (!strcmp(argv[i], "--gen") && has) a.gen = argv[++i];
+    else if (!strcmp(argv[i], "--qgen") && has) a.qgen = argv[++i];
+    else if (!strcmp(argv[i], "--tune") && has) a.tune = argv[++i];
+    else if (!strcmp(argv[i], "--threads") && has) a.threads = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--repeat") && has) a.repeat = std::max(1, atoi(argv[++i]));
+    else if (!strcmp(argv[i], "--spmd") && has) a.spmd = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--cache")) a.cache = true;
+    else if (!strcmp(argv[i], "--no-cache")) a.cache = false;
+    else if (!strcmp(argv[i], "--json")) a.json = true;
+    else if (!strcmp(argv[i], "--sort-rows")) a.sort_rows = true;
+    else if (!strcmp(argv[i], "--no-relabel")) a.relabel = false;
+  }
+  int rc = 0;
+  if (a.spmd >= 1) {
+    // single-process multi-GPU (the ncclCommInitAll bootstrap): one thread per rank
+    try {
+      if (world->size() != 1) fail("--spmd runs the whole job in one process (launch one rank)");
+      if (a.numGPU <= 0) fail("-gn must be >= 1 (the reference divides by it, main.cu:227)");
+      auto comms = make_thread_comms(a.spmd);
+      // (one rank: RCCL only when asked for, like maybe_upgrade_rccl: a one-rank communicator
+      // still runs every device collective)
+      if (a.algo != "cpu" && (a.comm == "rccl" || (a.comm == "auto" && a.spmd > 1))) {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) fail("no GPU visible (use --algo cpu)");
+        std::vector<int> devs(a.spmd);
+        for (int r = 0; r < a.spmd; ++r) devs[r] = (r % a.numGPU) % ndev;
+        comms = upgrade_thread_comms_rccl(std::move(comms), devs);
+      }
+      std::vector<int> rcs(a.spmd, 0);
+      std::vector<std::thread> th;
+      for (int r = 0; r < a.spmd; ++r)
+        th.emplace_back([&, r] { rcs[r] = rank_main(a, std::move(comms[r]), true); });
+      for (auto& t : th) t.join();
+      for (int x : rcs) rc = std::max(rc, x);
+    } catch (const std::exception& e) {
+      fprintf(stderr, "msbfs: %s\n", e.what());
+      rc = EXIT_FAILURE;
+    }
+  } else {
+    rc = rank_main(a, std::move(world), false);
+  }
+  finalize_world();
+  return rc;
 }

@@ -130,6 +130,9 @@ class Solver {
   // of reached vertices, i.e. 2x the Graph500 traversed-edge count) are written to host memory.
   virtual void run(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t* F,
                    int64_t* edges2, RunStats* st, hipStream_t stream) = 0;
+  // Groups one solver pass handles at once (bit-parallel: 64*W; per-group solvers run any
+  // number in one call). Callers that overlap work between passes split runs at this size.
+  virtual int64_t pass_groups() const { return INT64_MAX; }
   // Algorithm tuning, "key=value,key=value" (bit-parallel solver: see bp::Tuning in
   // kernels/bitpar/solver.hpp). Unknown keys are errors; solvers without tuning reject any.
   virtual void tune(const std::string& spec) {

@@ -86,6 +86,7 @@ class BitparSolver final : public Solver {
   void run(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t* F, int64_t* edges2,
            RunStats* st, hipStream_t stream) override;
   void tune(const std::string& spec) override { tun_.parse(spec); }
+  int64_t pass_groups() const override { return 64 * (int64_t)std::min(maxW_, opt.max_words); }
 
   int64_t hybrid_max_groups() const override { return 64 * (int64_t)maxW_; }
   void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,

@@ -6,6 +6,13 @@
 //    atomicCAS(-1 -> L+1) claims; bottom-up scans the shrinking list of unvisited vertices and stops
 //    at the first neighbour on level L (hubs get a whole wave). F(U) = sum_L L*|frontier_L| is
 //    accumulated from the per-level queue lengths, so no distance array is ever reduced or copied.
+//    Every frontier is appended to ONE visit-order array (level L's frontier is a contiguous
+//    slice), which gives (a) device-driven level batches on low-degree graphs: up to 64 top-down
+//    levels per host round trip, each level reading its slice bounds from device counter slots
+//    written by the previous level (road grid: thousands of levels, one host sync per batch
+//    instead of three per level as in main.cu:61-71), and (b) a reset of the distance array by
+//    scattering -1 over the visited prefix when a group reached few vertices, instead of the
+//    4n-byte refill per group (the reference rebuilds and copies n ints per query, main.cu:42-53).
 //  * SweepSolver — the reference algorithm (BFSKernal main.cu:16-38: one thread per vertex, every
 //    level rescans all n distances; GPUMultiSourceBFS main.cu:40-73) done MI355X-style: device
 //    source scatter instead of a host-built n-int array + H2D copy (main.cu:44-53), a pinned
@@ -33,6 +40,70 @@ struct HostCtr {
 };
 
 constexpr int kWaves = kBlock / 64;
+
+// Device-driven level batches (low-degree graphs): slot j describes level j's frontier, the
+// slice ord[lo, lo + nf); the kernel of level j appends level j+1's vertices after it and fills
+// slot j+1. stop = 1: the level's push -> pull test fired, the host continues from there.
+struct alignas(128) LevelSlot {
+  unsigned long long lo;
+  uint32_t nf;
+  uint32_t stop;
+  unsigned long long ef;  // degree sum of the frontier
+  uint32_t pad[26];
+};
+constexpr int kMaxBatch = 64;
+
+// one top-down level of a device-driven batch: thread per frontier vertex (max degree <= 64)
+__global__ __launch_bounds__(kBlock) void k_td_dd(int32_t* ord, LevelSlot* slots, int j,
+                                                  int32_t level0, const int64_t* rowptr,
+                                                  const int32_t* col, int32_t* dist,
+                                                  unsigned long long ef_stop) {
+  __shared__ LdsQueue q;
+  __shared__ unsigned long long scratch[kWaves];
+  const LevelSlot cur = slots[j];
+  if (cur.nf == 0) return;  // frontier died (or an earlier level stopped the batch)
+  if (j > 0 && cur.ef > ef_stop) {  // the host would pull here: stop the batch at this level
+    if (blockIdx.x == 0 && threadIdx.x == 0) slots[j].stop = 1u;
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) slots[j + 1].lo = cur.lo + cur.nf;
+  q_init(q);
+  __syncthreads();
+  int32_t* out = ord + cur.lo + cur.nf;
+  const int32_t nl = level0 + j + 1;  // slot 0 is level level0
+  unsigned long long ef = 0;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock; b < cur.nf; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = b + threadIdx.x;
+    int64_t e = 0, end = 0;
+    if (i < cur.nf) {
+      const int32_t u = ord[cur.lo + i];
+      e = rowptr[u];
+      end = rowptr[u + 1];
+    }
+    // one edge per step for every thread (block-uniform steps: the queue flushes every step)
+    while (__syncthreads_or(e < end)) {
+      bool app = false;
+      int32_t v = 0;
+      if (e < end) {
+        v = col[e++];
+        if (dist[v] < 0) app = atomicCAS(&dist[v], -1, nl) == -1;
+        if (app) ef += (unsigned long long)(rowptr[v + 1] - rowptr[v]);
+      }
+      q_push(q, app, v);
+      q_flush(q, out, &slots[j + 1].nf, kBlock, false);
+    }
+  }
+  q_flush(q, out, &slots[j + 1].nf, 0, true);
+  block_sum_add(ef, &slots[j + 1].ef, scratch);
+}
+
+// dist[ord[i]] = -1 for the visited prefix (the reset when a group reached few vertices)
+__global__ __launch_bounds__(kBlock) void k_reset_visited(const int32_t* ord, int64_t cnt,
+                                                          int32_t* dist) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < cnt;
+       i += (int64_t)gridDim.x * kBlock)
+    dist[ord[i]] = -1;
+}
 
 __global__ __launch_bounds__(kBlock) void k_init(const int32_t* src, int64_t ns, int64_t n,
                                                  const int64_t* rowptr, int32_t* dist, int32_t* fl,
@@ -270,8 +341,9 @@ class DistSolver final : public Solver {
   explicit DistSolver(const DeviceGraph& g) : g_(g) {
     const int64_t n = std::max<int64_t>(g.n, 1);
     dist_.alloc((size_t)n * sizeof(int32_t));
+    MSBFS_HIP_CHECK(hipMemset(dist_.p, 0xFF, dist_.bytes));
+    ord_.alloc((size_t)n * sizeof(int32_t));
     for (int i = 0; i < 2; ++i) {
-      fl_[i].alloc((size_t)n * sizeof(int32_t));
       ul_[i].alloc((size_t)n * sizeof(int32_t));
       ulw_[i].alloc((size_t)n * sizeof(int32_t));
     }
@@ -280,6 +352,8 @@ class DistSolver final : public Solver {
     scan_tmp_.alloc(scan_bytes_);
     ctr_.alloc(sizeof(Ctr));
     hctr_ = std::make_unique<PinnedBuf>(sizeof(Ctr));
+    slots_.alloc((size_t)(kMaxBatch + 1) * sizeof(LevelSlot));
+    hslots_ = std::make_unique<PinnedBuf>((size_t)(kMaxBatch + 1) * sizeof(LevelSlot));
   }
 
   void run(int64_t K, const int64_t* qoff, const int32_t* qids, int64_t* F, int64_t* edges2,
@@ -288,36 +362,91 @@ class DistSolver final : public Solver {
     int64_t maxs = 1;
     for (int64_t k = 0; k < K; ++k) maxs = std::max(maxs, qoff[k + 1] - qoff[k]);
     src_.ensure((size_t)maxs * sizeof(int32_t));
+    // device-driven top-down batches where every frontier vertex has few edges (road-like)
+    const bool dd = g_.max_degree <= 64 && opt.force_dir != 2;
     for (int64_t k = 0; k < K; ++k) {
       const int64_t ns = qoff[k + 1] - qoff[k];
-      MSBFS_HIP_CHECK(hipMemsetAsync(dist_.p, 0xFF, (size_t)std::max<int64_t>(n, 1) * 4, s));
+      // reset: the previous group's visited vertices are ord[0, visited_); scatter -1 over them
+      // when that is cheaper than refilling all n ints
+      if (visited_ * 8 < n) {
+        if (visited_)
+          k_reset_visited<<<grid_for(visited_, kBlock, 4096), kBlock, 0, s>>>(
+              ord_.as<int32_t>(), visited_, dist_.as<int32_t>());
+      } else {
+        MSBFS_HIP_CHECK(hipMemsetAsync(dist_.p, 0xFF, (size_t)std::max<int64_t>(n, 1) * 4, s));
+      }
+      visited_ = 0;
       MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
       if (ns) {
         MSBFS_HIP_CHECK(hipMemcpyAsync(src_.p, qids + qoff[k], ns * sizeof(int32_t),
                                        hipMemcpyHostToDevice, s));
         k_init<<<grid_for(ns, kBlock), kBlock, 0, s>>>(src_.as<int32_t>(), ns, n, g_.rowptr,
-                                                       dist_.as<int32_t>(), fl_[0].as<int32_t>(),
+                                                       dist_.as<int32_t>(), ord_.as<int32_t>(),
                                                        ctr_.as<Ctr>(), g_.old2new);
         MSBFS_HIP_CHECK(hipGetLastError());
       }
       HostCtr c = read(s);
-      int64_t nf = c.fl2, ef = (int64_t)c.ef2, Fk = 0, E2 = ef;
+      // frontier of level L = ord[lo, lo + nf)
+      int64_t lo = 0, nf = c.fl2, ef = (int64_t)c.ef2, Fk = 0, E2 = ef;
       int64_t na = n, ea = g_.nnz, nu = 0, nuw = 0;
-      int fc = 0, uc = 0;
+      int uc = 0;
       bool bottom_up = false, have_ul = false;
       int32_t L = 0;
+      int batch = 4;
       while (nf > 0) {
         if (opt.force_dir == 1) bottom_up = false;
         else if (opt.force_dir == 2) bottom_up = L > 0;
         else if (!bottom_up) bottom_up = (double)ef > (double)ea / opt.alpha;
         else bottom_up = !((double)nf < (double)na / opt.beta);
+        if (dd && !bottom_up) {
+          // ---- up to `batch` top-down levels, one host round trip
+          MSBFS_HIP_CHECK(hipMemsetAsync(slots_.p, 0, slots_.bytes, s));
+          LevelSlot s0{};
+          s0.lo = (unsigned long long)lo;
+          s0.nf = (uint32_t)nf;
+          s0.ef = (unsigned long long)ef;
+          MSBFS_HIP_CHECK(hipMemcpyAsync(slots_.p, &s0, sizeof(s0), hipMemcpyHostToDevice, s));
+          const unsigned long long ef_stop =
+              opt.force_dir == 1 ? ~0ull
+                                 : (unsigned long long)std::max(0.0, std::min((double)ea / opt.alpha, 1.8e19));
+          const int grid = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
+          trace::Range range_batch("dist L%d-%d TD batch", L + 1, L + batch);
+          for (int j = 0; j < batch; ++j)
+            k_td_dd<<<grid, kBlock, 0, s>>>(ord_.as<int32_t>(), slots_.as<LevelSlot>(), j, L,
+                                            g_.rowptr, g_.col, dist_.as<int32_t>(), ef_stop);
+          // (slot j describes level L + j)
+          MSBFS_HIP_CHECK(hipGetLastError());
+          MSBFS_HIP_CHECK(hipMemcpyAsync(hslots_->p, slots_.p, (size_t)(batch + 1) * sizeof(LevelSlot),
+                                         hipMemcpyDeviceToHost, s));
+          MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+          const LevelSlot* h = hslots_->as<LevelSlot>();
+          int real = 0;  // levels that expanded
+          while (real < batch && h[real].nf > 0 && !h[real].stop) {
+            Fk += (int64_t)(L + real + 1) * (int64_t)h[real + 1].nf;
+            E2 += (int64_t)h[real + 1].ef;
+            ++real;
+          }
+          if (st) {
+            st->td_levels += real;
+            st->levels += real;
+          }
+          L += real;
+          lo = (int64_t)h[real].lo;
+          nf = h[real].nf;
+          ef = (int64_t)h[real].ef;
+          if (real == batch) batch = std::min(batch * 2, kMaxBatch);
+          if (real < batch && h[real].stop) bottom_up = true;  // the batch stopped for a pull
+          if (nf == 0) break;
+          if (!bottom_up) continue;
+        }
         MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
+        int32_t* out = ord_.as<int32_t>() + lo + nf;  // the next frontier follows this one
         if (!bottom_up) {
-          frontier_degree_scan(g_.rowptr, fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(),
+          frontier_degree_scan(g_.rowptr, ord_.as<int32_t>() + lo, nf, offs_.as<int64_t>(),
                                scan_tmp_.p, scan_bytes_, s);
           k_td<<<grid_for(ef, kBlock, 8192), kBlock, 0, s>>>(
-              fl_[fc].as<int32_t>(), nf, offs_.as<int64_t>(), g_.rowptr, g_.col,
-              dist_.as<int32_t>(), L + 1, fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>());
+              ord_.as<int32_t>() + lo, nf, offs_.as<int64_t>(), g_.rowptr, g_.col,
+              dist_.as<int32_t>(), L + 1, out, ctr_.as<Ctr>());
           MSBFS_HIP_CHECK(hipGetLastError());
           if (st) st->td_levels++;
         } else {
@@ -336,11 +465,11 @@ class DistSolver final : public Solver {
           if (nu)
             k_bu<<<grid_for(nu, kBlock), kBlock, 0, s>>>(
                 ul_[uc].as<int32_t>(), nu, g_.rowptr, g_.col, dist_.as<int32_t>(), L,
-                ul_[uc ^ 1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>());
+                ul_[uc ^ 1].as<int32_t>(), out, ctr_.as<Ctr>());
           if (nuw)
             k_bu_wide<<<grid_for(nuw, kBlock / 64), kBlock, 0, s>>>(
                 ulw_[uc].as<int32_t>(), nuw, g_.rowptr, g_.col, dist_.as<int32_t>(), L,
-                ulw_[uc ^ 1].as<int32_t>(), fl_[fc ^ 1].as<int32_t>(), ctr_.as<Ctr>());
+                ulw_[uc ^ 1].as<int32_t>(), out, ctr_.as<Ctr>());
           MSBFS_HIP_CHECK(hipGetLastError());
           uc ^= 1;
           if (st) st->bu_levels++;
@@ -352,14 +481,15 @@ class DistSolver final : public Solver {
           na = nu + nuw;
           ea = (int64_t)c.eu2;
         }  // after a top-down level the lists may hold visited vertices: dropped lazily
+        lo += nf;
         nf = c.fl2;
         ef = (int64_t)c.ef2;
         Fk += (int64_t)(L + 1) * nf;
         E2 += ef;
-        fc ^= 1;
         ++L;
         if (st) st->levels++;
       }
+      visited_ = lo + nf;  // every visited vertex sits in ord[0, lo + nf)
       F[k] = Fk;
       if (edges2) edges2[k] = E2;
     }
@@ -373,9 +503,10 @@ class DistSolver final : public Solver {
     return HostCtr{c->fl2.v, c->ul2.v, c->ulw2.v, c->updated.v, c->ef2.v, c->eu2.v};
   }
   const DeviceGraph& g_;
-  DevBuf dist_, fl_[2], ul_[2], ulw_[2], offs_, scan_tmp_, ctr_, src_;
+  DevBuf dist_, ord_, ul_[2], ulw_[2], offs_, scan_tmp_, ctr_, src_, slots_;
   size_t scan_bytes_ = 0;
-  std::unique_ptr<PinnedBuf> hctr_;
+  int64_t visited_ = 0;  // vertices the last group reached (ord[0, visited_) to reset)
+  std::unique_ptr<PinnedBuf> hctr_, hslots_;
 };
 
 class SweepSolver final : public Solver {

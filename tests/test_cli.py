@@ -147,3 +147,36 @@ def test_cli_baseline_config1_serial_cpu(msbfs_pkg):
     assert js["F"] == F and js["K"] == 4 and js["n"] == 1000
     k = int(np.argmin(F))
     assert r.stdout.splitlines()[2] == f"Query number (k) with minimum F value: {k + 1}"
+
+
+@pytest.mark.parametrize("ranks", [1, 2, 3, 5])
+def test_cli_spmd_threads_world_size_invariance(tmp_path, msbfs_pkg, ranks):
+    """--spmd N: the whole job in ONE process, N ranks as N threads (the in-process ThreadComm:
+    shared-memory broadcasts, all-reduces, all-to-all; SURVEY C8 single-process mode). Same
+    report and F vector as the oracle for every N, idle ranks included (K=4 < 5)."""
+    m = msbfs_pkg
+    g = m.Graph.rmat(10, 8, 4)
+    gp, qp = str(tmp_path / "r.bin"), str(tmp_path / "q.bin")
+    g.write(gp)
+    qs = m.QuerySet.random(g.n, 4, 2, 3)
+    qs.write(qp)
+    ref = m.cpu_bfs(g, qs)
+    k = m.argmin_first(ref.F)
+    r = _run([_cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo", "cpu", "--spmd", str(ranks),
+              "--json"], {"MSBFS_NO_MPI": "1"})
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert len(lines) == 8  # the 7-line report once (rank 0) + the JSON line
+    assert lines[2] == f"Query number (k) with minimum F value: {k + 1}"
+    assert lines[3] == f"Minimum F value: {ref.F[k]}"
+    import json
+    js = json.loads(lines[7])
+    assert js["F"] == list(map(int, ref.F)) and js["ranks"] == ranks and js["comm"] == "threads"
+
+
+def test_cli_spmd_fault_takes_process_down(msbfs_pkg):
+    """A failure in one rank-thread ends the whole single-process job with an error (its peers
+    would otherwise wait in a collective forever)."""
+    r = _run([_cli(msbfs_pkg), "--gen", "rmat:9:8:2", "--qgen", "20:3:5", "-gn", "1", "--algo",
+              "cpu", "--spmd", "3"], {"MSBFS_NO_MPI": "1", "MSBFS_FAULT": "compute:1"})
+    assert r.returncode != 0 and "injected fault: compute on rank 1" in r.stderr

@@ -138,3 +138,37 @@ def test_cli_gpu_hybrid_coded_exchange(tmp_path, msbfs_pkg, ranks, K, comm):
               "bitpar", "--dist", "hybrid-coded", "--comm", comm, "--json"])
     js = _check(r, ref, m, ranks)
     assert js["comm"] == comm
+
+
+@pytest.mark.parametrize("spmd,comm,dist,K", [(1, "rccl", "roundrobin", 2100),
+                                              (1, "rccl", "hybrid", 200),
+                                              (2, "auto", "hybrid", 300),
+                                              (3, "auto", "roundrobin", 700)])
+def test_cli_gpu_spmd(tmp_path, msbfs_pkg, spmd, comm, dist, K):
+    """--spmd N: the job in one process, ranks as threads. One rank with --comm rccl makes its
+    communicator with ncclCommInitAll (the single-process multi-GPU bootstrap) and runs the
+    round-robin passes (K = 2100: several 64*W-group passes) with their packed MIN reductions
+    issued asynchronously on the communicator's stream while the next pass computes;
+    --repeat 3 re-runs the timed region on the same persistent buffers. Several threads on the
+    box's one GPU use the in-process ThreadComm (device all-to-all by peer copies)."""
+    m = msbfs_pkg
+    g, qs, gp, qp = _files(tmp_path, m, K, 4)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    r = _run([_cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo", "bitpar", "--spmd", str(spmd),
+              "--comm", comm, "--dist", dist, "--repeat", "3", "--json"], {"MSBFS_NO_MPI": "1"})
+    js = _check(r, ref, m, spmd)
+    assert js["comm"] == ("rccl" if comm == "rccl" else "threads")
+    assert js["traversed_edges"] == int(ref.edges.sum())
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+def test_cli_gpu_rccl_repeat_multipass(tmp_path, msbfs_pkg):
+    """One-rank RCCL over MPI with several solver passes and --repeat 3: the asynchronous
+    per-pass reductions and the persistent device scratch give the exact answer every time."""
+    m = msbfs_pkg
+    g, qs, gp, qp = _files(tmp_path, m, 1500, 3)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    r = _run([MPIEXEC, "-n", "1", _cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo", "bitpar",
+              "--comm", "rccl", "--repeat", "3", "--json"])
+    js = _check(r, ref, m, 1)
+    assert js["comm"] == "rccl"

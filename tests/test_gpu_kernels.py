@@ -449,3 +449,28 @@ def test_bitpar_tuning_rejects_unknown_keys(msbfs_pkg):
         with pytest.raises(m.native.MsbfsError):
             s.tune("gamma=1")
     g.close()
+
+
+def test_dist_device_batches_and_reset(msbfs_pkg):
+    """The per-group distance solver keeps every frontier in one visit-order array: low-degree
+    graphs run device-driven batches of top-down levels (slice bounds in device slots, one host
+    round trip per batch; uniform graphs stop a batch where the host pulls), and the distance
+    array is reset by scattering -1 over the visited prefix after groups that reached few
+    vertices (many small components) or refilled after large ones. F and the traversed-edge
+    counts equal the CPU oracle's, for the distance solver and its top-down-only variant, over
+    repeated runs of the same solver."""
+    m = msbfs_pkg
+    graphs = [m.Graph.grid(90, 110, 0.65, 0, 3), m.Graph.grid(60, 60, 0.9, 30, 2),
+              m.Graph.uniform(20000, 160000, 5), m.Graph.uniform(6000, 3500, 6),
+              m.Graph.rmat(12, 16, 3)]
+    for gi, g in enumerate(graphs):
+        dg = g.to_device(0)
+        qs = m.QuerySet.random(g.n, 24, 2, seed=gi + 1)
+        ref = m.cpu_bfs(g, qs, count_edges=True)
+        for algo in ("dist", "topdown"):
+            with m.Solver(dg, algo) as s:
+                for _ in range(2):
+                    r = s.run(qs, count_edges=True)
+                    assert np.array_equal(r.F, ref.F), (gi, algo)
+                    assert np.array_equal(r.edges, ref.edges), (gi, algo)
+        dg.close()
