@@ -109,6 +109,7 @@ def main() -> int:
     qs = msbfs.QuerySet.random(g.n, args.groups, args.group_size, args.qseed)
     solver = msbfs.Solver(g, args.algo, max_groups=qs.K, alpha=args.alpha, beta=args.beta,
                           wide_degree=args.wide_degree, max_words=args.max_words)
+    solver.prepare()
     # Every rank must pick the same candidates (hybrid and round-robin call different
     # collectives), but hybrid_max_groups() depends on the free HBM each rank saw: agree on it.
     # (the hybrid exchange moves rows by vertex id: every rank must number vertices alike)

@@ -273,6 +273,7 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
       }
       if (a.json) solver->opt.count_edges = true;
       if (!a.tune.empty()) solver->tune(a.tune);
+      solver->prepare(stream);  // graph-derived tables: preprocessing, not computation
       MSBFS_HIP_CHECK(hipDeviceSynchronize());
     }
     // Every rank must take the same branch (the two modes call different collectives), but

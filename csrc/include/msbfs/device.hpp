@@ -133,6 +133,9 @@ class Solver {
   // Groups one solver pass handles at once (bit-parallel: 64*W; per-group solvers run any
   // number in one call). Callers that overlap work between passes split runs at this size.
   virtual int64_t pass_groups() const { return INT64_MAX; }
+  // Build graph-derived tables and worst-case scratch now (before a timed region) instead of on
+  // the first run.
+  virtual void prepare(hipStream_t stream) { (void)stream; }
   // Algorithm tuning, "key=value,key=value" (bit-parallel solver: see bp::Tuning in
   // kernels/bitpar/solver.hpp). Unknown keys are errors; solvers without tuning reject any.
   virtual void tune(const std::string& spec) {

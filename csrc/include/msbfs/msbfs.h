@@ -110,6 +110,9 @@ int msbfs_solver_set_options(msbfs_solver s, const msbfs_options* o);
  * Unknown keys or bad values fail with an error; other solvers accept only an empty spec. The
  * process-wide defaults come from MSBFS_TUNE (same syntax, read once, echoed on stderr). */
 int msbfs_solver_tune(msbfs_solver s, const char* spec);
+/* Build graph-derived tables and worst-case scratch now instead of in the first run (the CLI
+ * calls it during preprocessing; optional). */
+int msbfs_solver_prepare(msbfs_solver s, void* stream);
 /* F[k] for k in [0,K); edges2 (nullable) = per-group sum of reached degrees (2x the Graph500
  * traversed-edge count). stream = hipStream_t or NULL for the null stream. */
 int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32_t* qids,

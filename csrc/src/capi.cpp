@@ -377,6 +377,13 @@ int msbfs_solver_set_options(msbfs_solver s, const msbfs_options* o) {
   });
 }
 
+int msbfs_solver_prepare(msbfs_solver s, void* stream) {
+  return guard([&] {
+    MSBFS_HIP_CHECK(hipSetDevice(s->graph->g.device));
+    s->impl->prepare((hipStream_t)stream);
+  });
+}
+
 int msbfs_solver_tune(msbfs_solver s, const char* spec) {
   return guard([&] {
     if (!spec) msbfs::fail("msbfs_solver_tune: null spec");

@@ -38,7 +38,7 @@
 #pragma once
 
 #include <chrono>
-#include <map>
+#include <vector>
 #include <memory>
 #include <string>
 
@@ -72,7 +72,11 @@ struct Tuning {
   int td_fused = 1;    // device-driven batches run the one-kernel k_td_fused levels
   int64_t td_bm = 65536;  // k_td_fused walks the frontier bitmap from this frontier size on
   int batch = 64;      // top-down levels per device-driven batch (1 = host-driven levels)
+  // fused batches: frontiers of at most `tail` vertices run in the one-workgroup tail kernel
+  // (k_td_tail, many levels per launch); 0 = off
+  int64_t tail = 2048;
   std::string dirs;    // forced per-level directions 'T'/'B' (tests, experiments)
+  int exp = 0;         // experimental kernel variants under A/B (bit mask; 0 = the defaults)
 
   void set(const std::string& key, const std::string& value);
   void parse(const std::string& spec);  // "k=v,k=v"
@@ -87,6 +91,8 @@ class BitparSolver final : public Solver {
            RunStats* st, hipStream_t stream) override;
   void tune(const std::string& spec) override { tun_.parse(spec); }
   int64_t pass_groups() const override { return 64 * (int64_t)std::min(maxW_, opt.max_words); }
+  // graph-derived tables and worst-case scratch, built before any timed run (bitpar_pull.hip)
+  void prepare(hipStream_t s) override;
 
   int64_t hybrid_max_groups() const override { return 64 * (int64_t)maxW_; }
   void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,
@@ -164,6 +170,8 @@ class BitparSolver final : public Solver {
   int level_td(Loop& S, hipStream_t s);
   template <int W, bool COUNT>
   void td_batch(Loop& S, RunStats* st, hipStream_t s);
+  template <int W>
+  void td_tail(Loop& S, RunStats* st, hipStream_t s);
   // ---- bitpar_pull.hip: one bottom-up level (returns the counter-slab rows it wrote)
   template <int W, bool COUNT>
   int level_bu(Loop& S, hipStream_t s);
@@ -269,10 +277,12 @@ class BitparSolver final : public Solver {
   int32_t plen_h_ = 0;
   DevBuf fbm_[2];   // frontier bitmaps of the fused levels (n bits each)
   DevBuf asnap_;    // any-visited bitmap at the start of a lazy batch's first pull level
-  std::map<int64_t, int32_t> code_bound_;
+  std::vector<int32_t> deg_bounds_;  // first id with degree < 2^k (relabelled graphs)
   const void* code_key_[2] = {nullptr, nullptr};
   int batch_next_ = 4;  // levels of the next device-driven batch (doubles while the frontier lives)
   DevBuf bctr_;  // (kBatch+1) Ctr slots, then (kBatch+1) x 16 alive words
+  DevBuf tail_out_;
+  std::unique_ptr<PinnedBuf> htail_;
   std::unique_ptr<PinnedBuf> hbctr_;
 };
 

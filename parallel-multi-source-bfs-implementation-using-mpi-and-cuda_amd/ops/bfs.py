@@ -55,6 +55,11 @@ class Solver:
         if tuning:
             self.tune(tuning)
 
+    def prepare(self, stream: Optional[int] = None) -> None:
+        """Build the graph-derived tables and worst-case scratch now, not in the first run."""
+        native.check(native.lib().msbfs_solver_prepare(self._h, C.c_void_p(stream) if stream
+                                                       else None))
+
     def tune(self, tuning) -> None:
         spec = tuning if isinstance(tuning, str) else ",".join(
             f"{k}={v}" for k, v in dict(tuning).items())
