@@ -3,14 +3,13 @@
 #include <unistd.h>
 
 #include <algorithm>
-#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
-#include <mutex>
 
 #include "msbfs/device.hpp"
+#include "thread_group.hpp"
 
 #ifdef MSBFS_HAVE_MPI
 #include <mpi.h>
@@ -88,33 +87,6 @@ class LocalComm final : public Comm {
 
 }  // namespace
 
-// ---- ThreadComm: ranks = threads of one process ------------------------------------------------
-struct ThreadGroup {
-  explicit ThreadGroup(int n) : size(n), ptrs(n), cptrs(n), vals(n), dvals(n), counts(n) {}
-  const int size;
-  std::mutex m;
-  std::condition_variable cv;
-  int arrived = 0;
-  uint64_t gen = 0;
-  // per-rank slots published between two barriers
-  std::vector<void*> ptrs;
-  std::vector<const void*> cptrs;
-  std::vector<uint64_t> vals;
-  std::vector<double> dvals;
-  std::vector<const std::vector<int64_t>*> counts;
-  void sync() {
-    std::unique_lock<std::mutex> l(m);
-    const uint64_t g = gen;
-    if (++arrived == size) {
-      arrived = 0;
-      ++gen;
-      cv.notify_all();
-    } else {
-      cv.wait(l, [&] { return gen != g; });
-    }
-  }
-};
-
 namespace {
 
 class ThreadComm final : public Comm {
@@ -125,10 +97,7 @@ class ThreadComm final : public Comm {
   std::string name() const override { return "threads"; }
   void barrier() override { g_->sync(); }
   void bcast_host(void* p, size_t bytes, int root) override {
-    if (rank_ == root) g_->cptrs[root] = p;
-    g_->sync();
-    if (rank_ != root && bytes) std::memcpy(p, g_->cptrs[root], bytes);
-    g_->sync();  // the root's buffer stays valid until every copy is done
+    tg_bcast(*g_, rank_, p, bytes, root);
   }
   void bcast_device(void* dptr, size_t bytes, int root, hipStream_t s) override {
     if (rank_ == root) g_->cptrs[root] = dptr;
@@ -142,57 +111,15 @@ class ThreadComm final : public Comm {
     }
     g_->sync();
   }
-  uint64_t allreduce_min_u64(uint64_t x) override {
-    g_->vals[rank_] = x;
-    g_->sync();
-    uint64_t r = x;
-    for (uint64_t v : g_->vals) r = std::min(r, v);
-    g_->sync();
-    return r;
-  }
-  void allreduce_sum_i64(int64_t* p, size_t n) override {
-    g_->cptrs[rank_] = p;
-    g_->sync();
-    std::vector<int64_t> t(n, 0);
-    for (int r = 0; r < g_->size; ++r) {
-      const int64_t* q = (const int64_t*)g_->cptrs[r];
-      for (size_t i = 0; i < n; ++i) t[i] += q[i];
-    }
-    g_->sync();  // everyone has read every input before anyone overwrites its own
-    if (n) std::memcpy(p, t.data(), n * 8);
-  }
-  double allreduce_max_f64(double x) override {
-    g_->dvals[rank_] = x;
-    g_->sync();
-    double r = x;
-    for (double v : g_->dvals) r = std::max(r, v);
-    g_->sync();
-    return r;
-  }
+  uint64_t allreduce_min_u64(uint64_t x) override { return tg_allreduce_min(*g_, rank_, x); }
+  void allreduce_sum_i64(int64_t* p, size_t n) override { tg_allreduce_sum(*g_, rank_, p, n); }
+  double allreduce_max_f64(double x) override { return tg_allreduce_max(*g_, rank_, x); }
   void allgather_u64(uint64_t x, std::vector<uint64_t>& out) override {
-    g_->vals[rank_] = x;
-    g_->sync();
-    out = g_->vals;
-    g_->sync();
-  }
-  // offset of rank r's block for rank `me` inside r's send buffer
-  int64_t send_offset(int r, int me) const {
-    int64_t o = 0;
-    for (int k = 0; k < me; ++k) o += (*g_->counts[r])[k];
-    return o;
+    tg_allgather(*g_, rank_, x, out);
   }
   void alltoallv_host_u64(const uint64_t* send, const std::vector<int64_t>& scount,
                           uint64_t* recv, const std::vector<int64_t>& rcount) override {
-    g_->cptrs[rank_] = send;
-    g_->counts[rank_] = &scount;
-    g_->sync();
-    int64_t ro = 0;
-    for (int r = 0; r < g_->size; ++r) {
-      if (rcount[r] != (*g_->counts[r])[rank_]) fail("threads all-to-all: count mismatch");
-      std::memcpy(recv + ro, (const uint64_t*)g_->cptrs[r] + send_offset(r, rank_), rcount[r] * 8);
-      ro += rcount[r];
-    }
-    g_->sync();
+    tg_alltoallv(*g_, rank_, send, scount, recv, rcount);
   }
   void alltoallv_device_u64(const uint64_t* send, const std::vector<int64_t>& scount,
                             uint64_t* recv, const std::vector<int64_t>& rcount,
@@ -209,7 +136,7 @@ class ThreadComm final : public Comm {
       if (rcount[r] != (*g_->counts[r])[rank_]) fail("threads all-to-all: count mismatch");
       if (rcount[r])
         MSBFS_HIP_CHECK(hipMemcpyPeerAsync(recv + ro, dev,
-                                           (const uint64_t*)g_->cptrs[r] + send_offset(r, rank_),
+                                           (const uint64_t*)g_->cptrs[r] + tg_send_offset(*g_, r, rank_),
                                            (int)g_->vals[r], rcount[r] * 8, s));
       ro += rcount[r];
     }

@@ -67,9 +67,8 @@ class Comm {
   std::vector<uint64_t> async_vals_;
 };
 
-// N ranks as N threads of one process (see above). Every thread owns one ThreadComm of the
-// same group; rank = thread index.
-struct ThreadGroup;
+// N ranks as N threads of one process (see above and thread_group.hpp). Every thread owns one
+// ThreadComm of the same group; rank = thread index.
 std::vector<std::unique_ptr<Comm>> make_thread_comms(int nranks);
 // Single-process multi-GPU: one RCCL communicator per device (ncclCommInitAll), each wrapped
 // around the thread comm of the same rank; returns the inputs unchanged without RCCL.

@@ -4,13 +4,16 @@
 // data race, main.cu:16-38). GPU AddressSanitizer is not available on the target
 // pool, so the sanitizers cover the native HOST code: the multi-threaded generators, the parallel
 // CSR build (count -> scan -> scatter over threads), the mmap loaders / writers and the CSR
-// sidecar cache, and the query-parallel CPU BFS. Every parallel result is compared with a
+// sidecar cache, the query-parallel CPU BFS and the in-process thread collectives of the
+// single-process multi-GPU mode. Every parallel result is compared with a
 // single-thread run, so a data race that changes a value fails the test even without TSan.
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <thread>
 #include <unistd.h>
 
+#include "../cli/thread_group.hpp"
 #include "msbfs/graph.hpp"
 
 using namespace msbfs;
@@ -24,10 +27,52 @@ static int fails = 0;
     }                                                              \
   } while (0)
 
+// The in-process communicator of the single-process multi-GPU mode (cli/thread_group.hpp): P
+// threads run many rounds of every collective back to back (the slots and the barrier are
+// reused immediately, the case a missing barrier would corrupt) and check every result.
+static void thread_group_selftest() {
+  const int P = 5, rounds = 300;
+  ThreadGroup g(P);
+  std::vector<int> bad(P, 0);
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; ++r)
+    th.emplace_back([&, r] {
+      for (int it = 0; it < rounds; ++it) {
+        int64_t buf[3] = {r == it % P ? (int64_t)it : -1, r == it % P ? (int64_t)(it * 7) : -1, 0};
+        tg_bcast(g, r, buf, 2 * sizeof(int64_t), it % P);
+        bad[r] += buf[0] != it || buf[1] != it * 7;
+        bad[r] += tg_allreduce_min(g, r, (uint64_t)(1000 + r * 13 + it)) != (uint64_t)(1000 + it);
+        bad[r] += tg_allreduce_max(g, r, (double)(r + it)) != (double)(P - 1 + it);
+        int64_t v[4] = {r, 1, it, -r};
+        tg_allreduce_sum(g, r, v, 4);
+        bad[r] += v[0] != P * (P - 1) / 2 || v[1] != P || v[2] != (int64_t)P * it ||
+                  v[3] != -P * (P - 1) / 2;
+        std::vector<uint64_t> all;
+        tg_allgather(g, r, (uint64_t)(r * r + it), all);
+        for (int k = 0; k < P; ++k) bad[r] += all[k] != (uint64_t)(k * k + it);
+        // all-to-all: rank r sends (j + 1 + it % 3) words of value r*100 + j to rank j
+        std::vector<int64_t> sc(P), rc(P);
+        std::vector<uint64_t> send, recv;
+        for (int j = 0; j < P; ++j) {
+          sc[j] = j + 1 + it % 3;
+          rc[j] = r + 1 + it % 3;
+          for (int64_t w = 0; w < sc[j]; ++w) send.push_back((uint64_t)(r * 100 + j));
+        }
+        recv.assign(P * (r + 1 + it % 3), ~0ull);
+        tg_alltoallv(g, r, send.data(), sc, recv.data(), rc);
+        for (int j = 0, o = 0; j < P; ++j)
+          for (int64_t w = 0; w < rc[j]; ++w) bad[r] += recv[o++] != (uint64_t)(j * 100 + r);
+      }
+    });
+  for (auto& t : th) t.join();
+  for (int r = 0; r < P; ++r) CHECK(bad[r] == 0);
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp";
   const std::string gp = dir + "/selftest_g.bin", qp = dir + "/selftest_q.bin";
   const int T = 8;
+  thread_group_selftest();
   // generators: threaded == serial
   EdgeList e1 = gen_rmat(12, 8, 5, 0.57, 0.19, 0.19, true, 1);
   EdgeList e8 = gen_rmat(12, 8, 5, 0.57, 0.19, 0.19, true, T);
