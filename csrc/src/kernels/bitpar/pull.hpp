@@ -454,154 +454,6 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
 }
 
 // ---------------------------------------------------------------------------------------------
-// First pull level (prefix pull, see k_push_tail), narrow vertices, probe-window form: every id
-// of a row prefix is < HUBW*32, so every probe is an LDS read of the hub bitmap snapshot. The G
-// lanes of a vertex load G consecutive column ids at once and probe them together; the visited
-// ones (about a third at level 2) are gathered 4 rows per round, ids broadcast inside the lane
-// group. One dependent round trip (column ids -> rows) per G prefix entries, instead of one per
-// 4 entries of the stepwise pull (k_bu_narrow PFX), which probed and gathered in lock step.
-// Same outputs as k_bu_narrow<..., FUSE, true, true>: row, counts, done bit, lists, anyvis.
-// ---------------------------------------------------------------------------------------------
-template <int W, int BT, int HUBW>
-__global__ __launch_bounds__(BT, 4) void k_bu_pfx(
-    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
-    const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
-    int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* actw2, int next_wide,
-    uint32_t* slabF, uint64_t* pacc, const int32_t* stamp, int32_t epoch, const int32_t* plen,
-    const uint32_t* snap) {
-  using L = Lay<W>;
-  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
-  static_assert(G >= 4, "probe windows of at least 4 ids");
-  constexpr int NWV = BT / 64, TILE = NWV * VPW;
-  constexpr int CR = 64;  // counter rows (the sparse spills of this level: no bank skew)
-  __shared__ LdsQueue qa, qf, qw;
-  __shared__ unsigned long long scratch[NWV];
-  __shared__ uint32_t hub[HUBW];
-  __shared__ uint32_t cnt[CR * W];
-  const uint32_t* pvis = snap ? snap : anyvis;
-  for (int i = threadIdx.x; i < HUBW; i += BT) hub[i] = pvis[i];
-  for (int i = threadIdx.x; i < CR * W; i += BT) cnt[i] = 0;
-  q_init(qa);
-  q_init(qf);
-  q_init(qw);
-  __syncthreads();
-  const int lane = lane_id(), slot = lane % G, sub = lane / G;
-  const int wv = threadIdx.x >> 6;
-  V<VW> am;
-#pragma unroll
-  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  unsigned long long eu = 0, ef = 0, ev = 0;
-  BitCounter<VW, 5> bc;
-  bc.zero();
-  int nadd = 0;
-  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nact; tb += (int64_t)gridDim.x * TILE) {
-    const int64_t idx = tb + wv * VPW + sub;
-    const bool valid = idx < nact;
-    int32_t v = 0;
-    V<VW> r = vzero<VW>(), acc = vzero<VW>(), unv = vzero<VW>();
-    int64_t beg = 0, end = 0;
-    uint32_t deg = 0;
-    bool lane_open = false, rnz = false;
-    if (valid) {
-      v = act[idx];
-      r = (snap && !any_visited(snap, v)) ? vzero<VW>() : ldv<VW>(R + (int64_t)v * W + slot * VW);
-      beg = rowptr[v];
-      deg = (uint32_t)(rowptr[v + 1] - beg);
-      end = beg + plen[v];
-      if (stamp[v] == epoch) {  // bits pushed from the tail frontier (k_push_tail)
-        acc = ldv<VW>(pacc + (int64_t)v * W + slot * VW);
-        stv<VW>(pacc + (int64_t)v * W + slot * VW, vzero<VW>());
-      }
-#pragma unroll
-      for (int j = 0; j < VW; ++j) {
-        unv.w[j] = ~r.w[j] & am.w[j];
-        lane_open |= unv.w[j] != 0;
-        rnz |= r.w[j] != 0;
-      }
-    }
-    bool g_go = valid && ((__ballot(lane_open) >> (sub * G)) & L::GBITS);
-    for (int64_t w0 = beg; __ballot(g_go && w0 < end); w0 += G) {
-      const bool act_w = g_go && w0 < end;
-      int32_t u = -1;
-      if (act_w && w0 + slot < end) u = col[w0 + slot];
-      const bool hit = u >= 0 && ((hub[u >> 5] >> (u & 31)) & 1u);
-      uint64_t hm = (__ballot(hit) >> (sub * G)) & L::GBITS;  // this group's visited ids
-      // rows of the visited ids, 4 per round; wave-uniform rounds (all lanes shuffle)
-      while (__ballot(hm != 0)) {
-        int32_t uu[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int b = hm ? __ffsll((unsigned long long)hm) - 1 : 0;
-          const int32_t x = __shfl(u, sub * G + b);
-          uu[q] = hm ? x : -1;
-          hm &= hm - 1;
-        }
-        V<VW> x[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          x[q] = uu[q] >= 0 ? ldv<VW>(R + (int64_t)uu[q] * W + slot * VW) : vzero<VW>();
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int j = 0; j < VW; ++j) acc.w[j] |= x[q].w[j];
-      }
-      bool cov = true;
-#pragma unroll
-      for (int j = 0; j < VW; ++j) cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
-      if (!((__ballot(!cov) >> (sub * G)) & L::GBITS)) g_go = false;  // group covered
-    }
-    V<VW> nw;
-    bool anynew = false, notfull = false;
-#pragma unroll
-    for (int j = 0; j < VW; ++j) {
-      nw.w[j] = acc.w[j] & unv.w[j];
-      anynew |= nw.w[j] != 0;
-      notfull |= (unv.w[j] & ~nw.w[j]) != 0;
-    }
-    if (valid) {
-      V<VW> nv;
-#pragma unroll
-      for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
-      stv<VW>(Wb + (int64_t)v * W + slot * VW, nv);
-    }
-    bc.add(nw);  // nw is zero for invalid lanes
-    if (++nadd == (1 << BitCounter<VW, 5>::D) - 1) {
-      bc.template spill_strided<CR>(cnt, slot);
-      nadd = 0;
-    }
-    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
-    const bool g_new = (bn >> (sub * G)) & L::GBITS;
-    const bool g_nf = (bf >> (sub * G)) & L::GBITS;
-    const bool leader = valid && slot == 0;
-    if (leader && !g_nf) set_done(done, v);
-    const bool keep = leader && g_nf, app = leader && g_new;
-    if (keep) eu += deg;
-    if (app) ef += deg;
-    const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
-    if (leader && g_first) {
-      atomicOr(&anyvis[v >> 5], 1u << (v & 31));
-      ev += deg;
-    }
-    q_push(qa, keep && (int)deg <= next_wide, v);
-    q_push(qw, keep && (int)deg > next_wide, v);
-    q_push(qf, app, v);
-    q_flush(qa, act2, &ctr->act2.v, TILE, false);
-    q_flush(qw, actw2, &ctr->actw2.v, TILE, false);
-    q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
-  }
-  q_flush(qa, act2, &ctr->act2.v, 0, true);
-  q_flush(qw, actw2, &ctr->actw2.v, 0, true);
-  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
-  block_sum_add(eu, &ctr->eu2.v, scratch);
-  block_sum_add(ef, &ctr->ef2.v, scratch);
-  block_sum_add(ev, &ctr->ev2.v, scratch);
-  bc.template spill_strided<CR>(cnt, slot);
-  __syncthreads();
-  uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
-  for (int i = threadIdx.x; i < 64 * W; i += BT) row[i] = cnt[i];
-}
-
-// ---------------------------------------------------------------------------------------------
 // Late pull levels, first pass: from the third bottom-up level on almost every
 // active vertex is covered by its first neighbour (rows sorted: the biggest hub first), and the
 // level is bound by the latency of its dependent loads (list entry -> row offsets -> first column
@@ -724,7 +576,7 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
                                            const uint32_t* hub, int32_t filter_from, int coop,
                                            int32_t* lst, const uint32_t* code,
                                            int32_t code_from, unsigned long long* wacc,
-                                           const uint32_t* snap, int exp) {
+                                           const uint32_t* snap) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
   constexpr int PB = VW == 2 ? 4 : 8;  // rows in flight per lane group in phase B
@@ -756,8 +608,8 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
   // each: OR the S lane groups' partial rows together and test coverage after every step of
   // PB*S rows; otherwise once per tile. Without early exit across chunks (coop = 0: the first
   // pull level, where hardly any row gets covered) the per-step reduction (3 x VW xor-shuffles)
-  // was most of the kernel's LDS instructions.
-  const bool each = coop != 0 || !(exp & 1);
+  // was most of the kernel's LDS instructions: RMAT-26 level-2 chunk pulls 6.63 -> 6.41 ms.
+  const bool each = coop != 0;
   for (int64_t t0 = beg; t0 < lim && !covered; t0 += T) {
     // ---- phase A: ids of this tile, filtered, compacted into lst[0..cnt)
     constexpr int Q = T / 64;
@@ -965,7 +817,7 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const uint64_t* R,
     const uint64_t* alive, const uint64_t* gmask, uint64_t* acc, const uint32_t* anyvis,
     int32_t filter_from, int coop, const uint32_t* code, int32_t code_from,
-    const uint32_t* snap, int exp) {
+    const uint32_t* snap) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G;
   __shared__ int32_t tile[BT / 64][T];
@@ -999,7 +851,7 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const int64_t lim = beg + uni32(d.len);
     if (c + cstep < cend) d = desc[c + cstep];  // next descriptor, in flight during the pull
     chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop,
-                           lst, code, code_from, wacc[threadIdx.x >> 6], snap, exp);
+                           lst, code, code_from, wacc[threadIdx.x >> 6], snap);
   }
 }
 

@@ -76,7 +76,6 @@ struct Tuning {
   // (k_td_tail, many levels per launch); 0 = off
   int64_t tail = 2048;
   std::string dirs;    // forced per-level directions 'T'/'B' (tests, experiments)
-  int exp = 0;         // experimental kernel variants under A/B (bit mask; 0 = the defaults)
 
   void set(const std::string& key, const std::string& value);
   void parse(const std::string& spec);  // "k=v,k=v"

@@ -203,20 +203,6 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
       // 4-neighbour steps: 122 VGPRs, no spills (8-neighbour steps spilled at the 128-VGPR
       // bound): RMAT-26 5.17 -> 4.96 ms (the full pulls of level 3 keep 8: 5.8 vs 6.8 ms)
-      if constexpr (FUSE && Lay<W>::G >= 4) {
-        if (tun_.exp & 2) {  // probe-window form (A/B)
-          k_bu_pfx<W, BT, kHubW><<<gn, BT, 0, s>>>(
-              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
-              done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
-              slabF<W>(rows), acc_[S.ac].as<uint64_t>(), stamp_.as<int32_t>(), epoch_, plen,
-              snap);
-          MSBFS_HIP_CHECK(hipGetLastError());
-          rows += gn;
-          goto narrow_done;
-        }
-      }
-      {
       auto kn = FUSE ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE, true, true, 4>
                      : k_bu_narrow<W, COUNT, BT, kHubW, false, true, true>;
       kn<<<gn, BT, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
@@ -226,8 +212,6 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                            next_wide, slabF<W>(rows), acc_[S.ac].as<uint64_t>(),
                            stamp_.as<int32_t>(), epoch_, plen, nullptr, snap);
       if (FUSE) rows += gn;
-      }
-    narrow_done:;
     } else if (hub_lds) {
       constexpr int BT = 1024;
       const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
@@ -274,12 +258,6 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                                         : k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false>)
                        : (filt ? k_bu_narrow<W, COUNT, kBlock, 0, false, true>
                                : k_bu_narrow<W, COUNT, kBlock, 0, false, false>);
-        // (A/B: fewer rows gathered per step on the unfiltered full-step levels)
-        if (FUSE && !filt && !short1) {
-          if (tun_.exp & 4) kn = k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 2>;
-          if (tun_.exp & 8) kn = k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 4, 0>;
-          if (tun_.exp & 16) kn = k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 4, 2>;
-        }
         kn<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
                                  sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                  fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
@@ -324,12 +302,12 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
           desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
           sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-          coop, codes, code_from, snap, tun_.exp);
+          coop, codes, code_from, snap);
     } else {
       k_bu_chunks<W, 256, kBlock, 0><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
           desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask,
           acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, coop, codes, code_from,
-          snap, tun_.exp);
+          snap);
     }
     MSBFS_HIP_CHECK(hipGetLastError());
     const int gw = grid_for(S.nactw, L::TILE, grid);
