@@ -106,7 +106,7 @@ void msbfs_graph_free(msbfs_graph g);
 int msbfs_solver_create(msbfs_graph g, int algo, int64_t max_groups, msbfs_solver* out);
 int msbfs_solver_set_options(msbfs_solver s, const msbfs_options* o);
 /* Algorithm tuning "key=value,key=value" (bit-parallel solver keys: gamma gamma2 pfx codes
- * code_deg lean lean_min lazy td_fused td_bm batch tail dirs; defaults are the measured best).
+ * code_deg lean lean_min lazy td_fused td_bm batch dirs; defaults are the measured best).
  * Unknown keys or bad values fail with an error; other solvers accept only an empty spec. The
  * process-wide defaults come from MSBFS_TUNE (same syntax, read once, echoed on stderr). */
 int msbfs_solver_tune(msbfs_solver s, const char* spec);

@@ -499,177 +499,3 @@ __global__ __launch_bounds__(kBlock) void k_td_fused(
 }  // namespace bp
 }  // namespace msbfs
 
-namespace msbfs {
-namespace bp {
-
-// ---------------------------------------------------------------------------------------------
-// Tail levels of high-diameter graphs in ONE workgroup: once the frontier is small (road grid:
-// the last ~1500 of 4640 levels have < 2048 frontier vertices), a level is a few dependent
-// round trips of work but cost a fixed 10-15 us as its own k_td_fused dispatch (launch, grid
-// drain, counter reduction every few levels). Here one 1024-thread block runs level after level
-// with __syncthreads() as the level barrier: no launches, no inter-block synchronisation (no
-// grid barrier to hang), counts and alive masks in LDS. It stops when the frontier dies, grows
-// beyond nf_max (the normal batches take over) or after max_levels; TailOut tells the host where.
-// Same per-level semantics as k_td_fused: the visited row is the claim (atomicOr return), new bits
-// go to the next accumulator, the reader clears the current one, only vis (= vis_[cur]) is kept.
-// ---------------------------------------------------------------------------------------------
-struct TailOut {
-  uint32_t levels;  // levels run
-  uint32_t nf;      // frontier size after them (0: BFS done)
-  uint32_t cur;     // 0: the frontier is in flA/accA, 1: in flB/accB
-  uint32_t pad;
-  unsigned long long ef, ev;  // its degree sum; degree sum of first visits (any group)
-};
-
-template <int W>
-__global__ __launch_bounds__(1024) void k_td_tail(
-    int32_t* flA, int32_t* flB, uint64_t* accA, uint64_t* accB, int64_t nf0,
-    const int64_t* rowptr, const int32_t* col, uint64_t* vis, const uint64_t* gmask,
-    uint64_t* alive_io, uint32_t* done, uint32_t* anyvis, int32_t* stamp, int32_t epoch0,
-    unsigned long long* F, uint32_t level0, int max_levels, int64_t nf_max, TailOut* out,
-    uint32_t* nf_log, unsigned long long* ef_log) {
-  using L = Lay<W>;
-  constexpr int BT = 1024, NWV = BT / 64;
-  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = NWV * VPW;
-  __shared__ uint32_t cnt[64 * W];            // new bits per group, this level
-  __shared__ unsigned long long fsum[64 * W]; // sum of level * count per group
-  __shared__ uint64_t alive[16];
-  __shared__ uint32_t nnext;                  // next frontier size
-  __shared__ unsigned long long evs, efs;
-  const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < 64 * W; i += BT) {
-    cnt[i] = 0;
-    fsum[i] = 0;
-  }
-  if (threadIdx.x < 16) alive[threadIdx.x] = alive_io[threadIdx.x];
-  if (threadIdx.x == 0) {
-    nnext = 0;
-    evs = 0;
-    efs = 0;
-  }
-  __syncthreads();
-  int64_t nf = nf0;
-  int cur = 0, lv = 0;
-  while (nf > 0 && nf <= nf_max && lv < max_levels) {
-    int32_t* fl = cur ? flB : flA;
-    int32_t* fn = cur ? flA : flB;
-    uint64_t* ac = cur ? accB : accA;
-    uint64_t* an = cur ? accA : accB;
-    const int32_t epoch = epoch0 + lv;
-    if (threadIdx.x == 0) nf_log[lv] = (uint32_t)nf;  // (level records for the host)
-    V<VW> amg;
-#pragma unroll
-    for (int j = 0; j < VW; ++j) amg.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-    unsigned long long ev = 0, efl = 0;
-    for (int64_t tb = 0; tb < nf; tb += TILE) {
-      const int64_t idx = tb + wv * VPW + sub;
-      const bool has = idx < nf;
-      int64_t e = 0, end = 0;
-      V<VW> fb = vzero<VW>();
-      if (has) {
-        const int32_t u = fl[idx];
-        e = rowptr[u];
-        end = rowptr[u + 1];
-        if (slot == 0) efl += (unsigned long long)(end - e);
-        // read and clear with one atomic: the bits were set by atomics of the previous level
-        // (performed beyond this CU's L1, which may still hold the line from two levels ago)
-#pragma unroll
-        for (int k = 0; k < VW; ++k)
-          fb.w[k] = atomicExch((unsigned long long*)&ac[(int64_t)u * W + slot * VW + k], 0ull);
-      }
-      while (__syncthreads_or(e < end)) {
-        const int32_t x = e < end ? col[e] : -1;
-        ++e;
-        bool push = false, first = false, full = true, was0 = true;
-        V<VW> nw = vzero<VW>();
-        if (x >= 0 && !is_done(done, x)) {
-          const int64_t xo = (int64_t)x * W + slot * VW;
-          const V<VW> r = ldv<VW>(vis + xo);
-#pragma unroll
-          for (int k = 0; k < VW; ++k) {
-            const uint64_t mm = fb.w[k] & ~r.w[k];
-            uint64_t now = r.w[k];
-            if (mm) {
-              const uint64_t ov = atomicOr((unsigned long long*)&vis[xo + k], mm);
-              const uint64_t oa = atomicOr((unsigned long long*)&an[xo + k], mm);
-              nw.w[k] = mm & ~ov;
-              now = ov | mm;
-              first |= oa == 0ull;
-              was0 &= ov == 0ull;
-              push = true;
-            }
-            full &= (~now & amg.w[k]) == 0;
-          }
-        }
-        // per-group counts of the bits this push claimed (few bits at tail levels: LDS atomics)
-#pragma unroll
-        for (int k = 0; k < VW; ++k)
-          for (uint64_t b = nw.w[k]; b; b &= b - 1)
-            atomicAdd(&cnt[(slot * VW + k) * 64 + __ffsll((unsigned long long)b) - 1], 1u);
-        const uint64_t bg = __ballot(push), bn = __ballot(!full);
-        const bool g_push = (bg >> (sub * G)) & L::GBITS;
-        const bool g_full = !((bn >> (sub * G)) & L::GBITS);
-        if (slot == 0 && g_push) {
-          const uint32_t bit = 1u << (x & 31);
-          bool app, fresh = false;
-          if constexpr (W == 1) {
-            app = first;
-            fresh = was0;
-            if (fresh) atomicOr(&anyvis[x >> 5], bit);
-          } else {
-            app = atomicExch(&stamp[x], epoch) != epoch;
-            if (!any_visited(anyvis, x)) fresh = !(atomicOr(&anyvis[x >> 5], bit) & bit);
-          }
-          if (g_full) set_done(done, x);
-          if (app) fn[atomicAdd(&nnext, 1u)] = x;  // (LDS counter: this block is the grid)
-          if (fresh) ev += (unsigned long long)(rowptr[x + 1] - rowptr[x]);
-        }
-      }
-    }
-    if (ev) atomicAdd(&evs, ev);
-    if (efl) atomicAdd(&efs, efl);
-    __syncthreads();  // level barrier: every push of this level is done
-    if (threadIdx.x == 0) {
-      ef_log[lv] = efs;  // degree sum of this level's frontier
-      efs = 0;
-    }
-    const uint32_t level = level0 + 1 + lv;
-    if (threadIdx.x < 64 * W) {  // W <= 16: one thread per group
-      const uint32_t c = cnt[threadIdx.x];
-      fsum[threadIdx.x] += (unsigned long long)c * level;
-      cnt[threadIdx.x] = 0;
-      const uint64_t m = __ballot(c != 0);  // groups with new vertices: next alive mask
-      if (lane == 0) alive[threadIdx.x >> 6] = m;
-    }
-    nf = nnext;
-    __syncthreads();
-    if (threadIdx.x == 0) nnext = 0;
-    cur ^= 1;
-    ++lv;
-    // the next level's readers need this level's global writes (same block: a block-scope
-    // fence orders them; no other block takes part)
-    __threadfence_block();
-    __syncthreads();
-  }
-  // degree sum of the frontier left for the host's direction test
-  if (threadIdx.x == 0) nf_log[lv] = (uint32_t)nf;
-  unsigned long long ef = 0;
-  const int32_t* flo = cur ? flB : flA;
-  if (nf > 0)
-    for (int64_t i = threadIdx.x; i < nf; i += BT) ef += (unsigned long long)(rowptr[flo[i] + 1] - rowptr[flo[i]]);
-  if (ef) atomicAdd(&efs, ef);
-  __syncthreads();
-  for (int i = threadIdx.x; i < 64 * W; i += BT)
-    if (fsum[i]) atomicAdd(&F[i], fsum[i]);
-  if (threadIdx.x < 16) alive_io[threadIdx.x] = alive[threadIdx.x];
-  if (threadIdx.x == 0) {
-    out->levels = (uint32_t)lv;
-    out->nf = (uint32_t)nf;
-    out->cur = (uint32_t)cur;
-    out->ef = efs;
-    out->ev = evs;
-  }
-}
-
-}  // namespace bp
-}  // namespace msbfs

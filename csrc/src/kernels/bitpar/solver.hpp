@@ -72,9 +72,6 @@ struct Tuning {
   int td_fused = 1;    // device-driven batches run the one-kernel k_td_fused levels
   int64_t td_bm = 65536;  // k_td_fused walks the frontier bitmap from this frontier size on
   int batch = 64;      // top-down levels per device-driven batch (1 = host-driven levels)
-  // fused batches: frontiers of at most `tail` vertices run in the one-workgroup tail kernel
-  // (k_td_tail, many levels per launch); 0 = off
-  int64_t tail = 2048;
   std::string dirs;    // forced per-level directions 'T'/'B' (tests, experiments)
 
   void set(const std::string& key, const std::string& value);
@@ -169,8 +166,6 @@ class BitparSolver final : public Solver {
   int level_td(Loop& S, hipStream_t s);
   template <int W, bool COUNT>
   void td_batch(Loop& S, RunStats* st, hipStream_t s);
-  template <int W>
-  void td_tail(Loop& S, RunStats* st, hipStream_t s);
   // ---- bitpar_pull.hip: one bottom-up level (returns the counter-slab rows it wrote)
   template <int W, bool COUNT>
   int level_bu(Loop& S, hipStream_t s);
@@ -280,8 +275,6 @@ class BitparSolver final : public Solver {
   const void* code_key_[2] = {nullptr, nullptr};
   int batch_next_ = 4;  // levels of the next device-driven batch (doubles while the frontier lives)
   DevBuf bctr_;  // (kBatch+1) Ctr slots, then (kBatch+1) x 16 alive words
-  DevBuf tail_out_;
-  std::unique_ptr<PinnedBuf> htail_;
   std::unique_ptr<PinnedBuf> hbctr_;
 };
 

@@ -86,80 +86,11 @@ int BitparSolver::level_td(Loop& S, hipStream_t s) {
 // batch reads its frontier size from counter slot i (slot 0 seeded from the host) and writes
 // slot i + 1; alive masks likewise. Levels after the frontier dies are no-ops (every kernel
 // sees a zero count). One copy of all slots afterwards restores the host's view.
-// Small frontiers of a fused-batch graph: levels in one workgroup (k_td_tail) until the frontier
-// dies or outgrows tun_.tail; one host round trip for all of them.
-template <int W>
-void BitparSolver::td_tail(Loop& S, RunStats* st, hipStream_t s) {
-  const Small sm = small();
-  constexpr int kTailLevels = 1 << 14;  // levels per launch (the host relaunches)
-  constexpr size_t kNfLog = (size_t)(kTailLevels + 2) * 4;  // (keeps ef_log 8-byte aligned)
-  constexpr size_t kLog = sizeof(TailOut) + kNfLog + (size_t)(kTailLevels + 1) * 8;
-  static_assert(sizeof(TailOut) % 8 == 0 && kNfLog % 8 == 0, "aligned logs");
-  tail_out_.ensure(kLog);
-  if (!htail_) htail_ = std::make_unique<PinnedBuf>(kLog);
-  TailOut* dout = tail_out_.as<TailOut>();
-  uint32_t* nf_log = (uint32_t*)(dout + 1);
-  unsigned long long* ef_log = (unsigned long long*)((char*)nf_log + kNfLog);
-  const uint32_t level0 = S.level;
-  const auto t0 = std::chrono::steady_clock::now();
-  trace::Range range_tail("bitpar L%u+ TD tail", level0 + 1);
-  k_td_tail<W><<<1, 1024, 0, s>>>(
-      fl_[S.fc].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(), acc_[S.ac].as<uint64_t>(),
-      acc_[S.ac ^ 1].as<uint64_t>(), S.nf, g_.rowptr, g_.col, vis_[S.cur].as<uint64_t>(),
-      sm.gmask, sm.alive[S.alv], done_.as<uint32_t>(), anyvis_.as<uint32_t>(),
-      stamp_.as<int32_t>(), epoch_ + 1, sm.F, level0, kTailLevels, tun_.tail, dout, nf_log,
-      ef_log);
-  MSBFS_HIP_CHECK(hipGetLastError());
-  MSBFS_HIP_CHECK(hipMemcpyAsync(htail_->p, tail_out_.p, sizeof(TailOut), hipMemcpyDeviceToHost, s));
-  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
-  const TailOut o = *htail_->as<TailOut>();
-  if (st && o.levels > 0) {  // the level logs, for the per-level records
-    MSBFS_HIP_CHECK(hipMemcpyAsync((char*)htail_->p + sizeof(TailOut), nf_log,
-                                   kLog - sizeof(TailOut), hipMemcpyDeviceToHost, s));
-    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
-  }
-  const uint32_t* hnf = (const uint32_t*)(htail_->as<TailOut>() + 1);
-  const unsigned long long* hef = (const unsigned long long*)((const char*)hnf + kNfLog);
-  epoch_ += (int32_t)o.levels + 1;
-  if (o.cur) {
-    S.fc ^= 1;
-    S.ac ^= 1;
-  }
-  S.old_stale = true;
-  S.level = level0 + o.levels;
-  S.nf = o.nf;
-  S.ef = (int64_t)o.ef;
-  S.ev += (int64_t)o.ev;
-  if (st && o.levels > 0) {  // per-level records; the launch's wall time split evenly
-    const double ms = std::chrono::duration<double, std::milli>(
-                          std::chrono::steady_clock::now() - t0).count() / o.levels;
-    for (uint32_t i = 0; i < o.levels; ++i) {
-      LevelRec rec;
-      rec.batch = (int32_t)st->batches;
-      rec.level = (int32_t)(level0 + 1 + i);
-      rec.dir = 'T';
-      rec.nf = hnf[i];
-      rec.ef = (int64_t)hef[i];
-      rec.nf_next = hnf[i + 1];
-      rec.active = hnf[i + 1];
-      rec.ms = ms;
-      st->recs.push_back(rec);
-    }
-    st->td_levels += o.levels;
-    st->levels += o.levels;
-  }
-}
-
 template <int W, bool COUNT>
 void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
   using L = Lay<W>;
   const int64_t n = g_.n;
   const Small sm = small();
-  if (fused_batches<COUNT>() && S.fsrc_acc && !S.lazy && S.weight_l1 && tun_.tail > 0 &&
-      S.nf <= tun_.tail) {
-    td_tail<W>(S, st, s);
-    return;
-  }
   int K = std::min<int>(batch_next_, tun_.batch);
   if (S.stop_level != 0xFFFFFFFFu) K = std::min<int64_t>(K, (int64_t)S.stop_level - S.level);
   K = std::max(K, 1);

@@ -39,15 +39,13 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "batch") {
     batch = (int)to_num(key, v);
     if (batch < 1 || batch > 64) fail("tuning: batch must be in [1, 64]");
-  } else if (key == "tail") {
-    tail = (int64_t)to_num(key, v);
   } else if (key == "dirs") {
     for (char c : v)
       if (c != 'T' && c != 'B' && c != '.') fail("tuning: dirs takes T, B or . per level");
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lazy td_fused td_bm batch tail dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lazy td_fused td_bm batch dirs)");
   }
 }
 

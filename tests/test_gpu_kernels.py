@@ -474,33 +474,3 @@ def test_dist_device_batches_and_reset(msbfs_pkg):
                     assert np.array_equal(r.F, ref.F), (gi, algo)
                     assert np.array_equal(r.edges, ref.edges), (gi, algo)
         dg.close()
-
-
-@pytest.mark.parametrize("tail", [0, 2048, 10**9])
-def test_bitpar_tail_levels_one_workgroup(msbfs_pkg, tail):
-    """Small frontiers of low-degree graphs run in the one-workgroup tail kernel (k_td_tail:
-    level after level inside one launch, __syncthreads as the level barrier). tail = 0 turns it
-    off, 10**9 runs every push level of the fused batches there. F equals the oracle's for every
-    setting, W = 1 / 4 / 16, over repeated runs; with pushes forced, the per-level records
-    (frontier sizes and degree sums, logged by the kernel) equal those of the batched levels."""
-    m = msbfs_pkg
-    graphs = [m.Graph.grid(90, 110, 0.65, 0, 3), m.Graph.grid(50, 50, 0.9, 20, 4),
-              m.Graph.uniform(60000, 200000, 7)]
-    for gi, g in enumerate(graphs):
-        dg = g.to_device(0)
-        for K in (1, 64, 200, 1024):
-            qs = m.QuerySet.random(g.n, K, 3, seed=K + gi)
-            ref = m.cpu_bfs(g, qs)
-            recs = {}
-            for t in (0, tail):
-                with m.Solver(dg, "bitpar", max_groups=K, force_dir=1,
-                              tuning={"tail": t}) as s:
-                    for _ in range(2):
-                        r = s.run(qs)
-                        assert np.array_equal(r.F, ref.F), (gi, K, t)
-                    recs[t] = [(x["level"], x["nf"], x["ef"], x["nf_next"])
-                               for x in s.level_trace()]
-            assert recs[0] == recs[tail], (gi, K)
-            with m.Solver(dg, "bitpar", max_groups=K, tuning={"tail": tail}) as s:
-                assert np.array_equal(s.run(qs).F, ref.F), (gi, K, tail)
-        dg.close()
