@@ -220,6 +220,32 @@ struct BitCounter {
   }
 };
 
+// Gate of a level of a device-driven pull batch (BitparSolver::bu_batch): level i reads counter
+// slot c (written by level i - 1, or seeded by the host for i = 0) and runs while the frontier
+// entering it is non-empty and the host loop's pull -> push test (levels(): nf < na / beta and
+// ef < ea / alpha, same double arithmetic) would keep pulling. Every kernel of the level
+// evaluates it at its start, so a closed level is a no-op. c == nullptr: always open.
+// The pull -> push test (Beamer et al. SC'12): switch back to push once the frontier is small
+// against the active vertices (beta) and its edges against theirs (alpha). One definition for
+// the host loop and the device gate, so both decide alike.
+__host__ __device__ inline bool keep_pulling(double nf, double ef, double na, double ea,
+                                             double beta, double alpha) {
+  return !(nf < na / beta && ef < ea / alpha);
+}
+struct BuGate {
+  const Ctr* c;
+  double beta, alpha;
+  int first;  // the batch's first level (the host already chose to pull)
+};
+__host__ __device__ inline bool bu_gate_eval(const Ctr& c, double beta, double alpha, int first) {
+  if (c.fl2.v == 0) return false;
+  return first || keep_pulling((double)c.fl2.v, (double)c.ef2.v,
+                               (double)c.act2.v + (double)c.actw2.v, (double)c.eu2.v, beta, alpha);
+}
+__device__ __forceinline__ bool bu_gate_open(const BuGate& g) {
+  return !g.c || bu_gate_eval(*g.c, g.beta, g.alpha, g.first);
+}
+
 // Sum the level's slab rows: block (word, row-group); lane = group bit. F += level * count
 // (`level` is the weight: 0 for a level another rank of the hybrid mode accounts for),
 // alive_next |= groups with count > 0 (one ballot + one atomicOr per word per row-group).
@@ -228,7 +254,9 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
                                                          const unsigned long long* slabE, int rows,
                                                          int rgroups, unsigned long long* F,
                                                          unsigned long long* E,
-                                                         uint64_t* alive_next, uint32_t level) {
+                                                         uint64_t* alive_next, uint32_t level,
+                                                         BuGate gate) {
+  if (!bu_gate_open(gate)) return;  // (uniform: no barrier skipped by part of the block)
   __shared__ unsigned long long pf[kWaves][64], pe[kWaves][64];
   const int word = blockIdx.x % W, rg = blockIdx.x / W;
   const int lane = lane_id(), wv = threadIdx.x >> 6;

@@ -220,8 +220,9 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t filter_from, int32_t* actw2,
     int next_wide, uint32_t* slabF, uint64_t* pacc, const int32_t* stamp, int32_t epoch,
-    const int32_t* plen, const uint32_t* nact_dev, const uint32_t* snap) {
+    const int32_t* plen, const uint32_t* nact_dev, const uint32_t* snap, BuGate gate) {
   static_assert(!PFX || HUBW > 0, "the prefix pull relies on the LDS hub bitmap");
+  if (!bu_gate_open(gate)) return;  // closed level of a device-driven batch (uniform)
   // snap (first pull level of a batch that did not clear its visited buffer, see start_batch):
   // the any-visited bitmap as of the level start. Probes read it (a vertex first visited during
   // this level may still have a stale row) and an own row it does not mark is all zero.
@@ -952,6 +953,21 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
     for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
   }
+}
+
+// counter slot 0 and alive mask 0 of a device-driven pull batch (bu_batch): the host's view
+// after the level before the batch
+__global__ void k_bu_seed(Ctr* c0, uint32_t nf, unsigned long long ef, uint32_t nact,
+                          uint32_t nactw, unsigned long long eu, const uint64_t* alive,
+                          uint64_t* alive0) {
+  if (threadIdx.x == 0) {
+    c0->fl2.v = nf;
+    c0->ef2.v = ef;
+    c0->act2.v = nact;
+    c0->actw2.v = nactw;
+    c0->eu2.v = eu;
+  }
+  if (threadIdx.x < 16) alive0[threadIdx.x] = alive[threadIdx.x];
 }
 
 }  // namespace bp

@@ -68,10 +68,14 @@ struct Tuning {
   // least lean_min vertices (RMAT-26 level 4: 2.48 -> 2.07 ms)
   int lean = 1;
   int64_t lean_min = 1 << 20;
+  int lean_level = 3;  // first pull level (1-based) that may run lean
   int lazy = 1;        // no per-batch fill of the visited buffer (see start_batch)
   int td_fused = 1;    // device-driven batches run the one-kernel k_td_fused levels
   int64_t td_bm = 65536;  // k_td_fused walks the frontier bitmap from this frontier size on
   int batch = 64;      // top-down levels per device-driven batch (1 = host-driven levels)
+  // pull levels from the third on run as device-driven batches (bu_batch) while the active lists
+  // hold at most bu_max vertices (0 = host-driven pull levels; needs batch > 1)
+  int64_t bu_max = 1 << 20;
   std::string dirs;    // forced per-level directions 'T'/'B' (tests, experiments)
 
   void set(const std::string& key, const std::string& value);
@@ -169,6 +173,10 @@ class BitparSolver final : public Solver {
   // ---- bitpar_pull.hip: one bottom-up level (returns the counter-slab rows it wrote)
   template <int W, bool COUNT>
   int level_bu(Loop& S, hipStream_t s);
+  template <int W, bool COUNT>
+  bool bu_batch_ok(const Loop& S) const;
+  template <int W, bool COUNT>
+  void bu_batch(Loop& S, RunStats* st, hipStream_t s);
   const int32_t* prefix_lens(int32_t H, hipStream_t s);
   const int32_t* first_nbr(hipStream_t s);
   int32_t code_bound(double min_deg);
@@ -240,7 +248,6 @@ class BitparSolver final : public Solver {
   // ---- fixed policy constants (formerly environment knobs; measured, see README)
   static constexpr double kFilterFrac = 0.5;  // filter unvisited neighbours while ev < frac*nnz
   static constexpr int kWideLater = 1024;     // wide split after the first bottom-up level
-  static constexpr int kLeanLevel = 3;        // first pull level (1-based) that may run lean
   static constexpr int kTdGrid = 1024;        // blocks of the device-driven batches' kernels
   static constexpr int kTdRed = 6;            // fused levels per k_level_reduce_multi launch
   // push -> pull threshold (Beamer's alpha) on graphs with max degree <= kSmallDeg (fused
@@ -274,6 +281,7 @@ class BitparSolver final : public Solver {
   std::vector<int32_t> deg_bounds_;  // first id with degree < 2^k (relabelled graphs)
   const void* code_key_[2] = {nullptr, nullptr};
   int batch_next_ = 4;  // levels of the next device-driven batch (doubles while the frontier lives)
+  int bu_next_ = 4;     // levels of the next device-driven pull batch (the last run's pull tail + 1)
   DevBuf bctr_;  // (kBatch+1) Ctr slots, then (kBatch+1) x 16 alive words
   std::unique_ptr<PinnedBuf> hbctr_;
 };

@@ -210,7 +210,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                            fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                            anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
                            next_wide, slabF<W>(rows), acc_[S.ac].as<uint64_t>(),
-                           stamp_.as<int32_t>(), epoch_, plen, nullptr, snap);
+                           stamp_.as<int32_t>(), epoch_, plen, nullptr, snap, BuGate{});
       if (FUSE) rows += gn;
     } else if (hub_lds) {
       constexpr int BT = 1024;
@@ -223,7 +223,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                            sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                            fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                            anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-                           next_wide, slabF<W>(rows), nullptr, nullptr, 0, nullptr, nullptr, snap);
+                           next_wide, slabF<W>(rows), nullptr, nullptr, 0, nullptr, nullptr, snap, BuGate{});
       if (FUSE) rows += gn;
     } else {
       const int gn = grid_for(S.nact, L::TILE, grid);
@@ -233,7 +233,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       // then most vertices are covered by their first neighbour (RMAT-26, 1024 groups: level
       // 4 3.1 -> 2.5 ms; level 3 prefers full steps: 6.5 vs 6.7 ms)
       const bool short1 = S.bu_levels >= 3 || W <= 4;
-      if (tun_.lean && !S.lean_off && FUSE && !filt && S.bu_levels >= kLeanLevel &&
+      if (tun_.lean && !S.lean_off && FUSE && !filt && S.bu_levels >= tun_.lean_level &&
           S.nact >= tun_.lean_min) {
         S.lean_ran = true;
         // lean first pass, then the regular pull over the vertices it could not finish
@@ -249,7 +249,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
             done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
             ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
             next_wide, slabF<W>(rows), nullptr, nullptr, 0, nullptr, &ctr_.as<Ctr>()->touched.v,
-            nullptr);
+            nullptr, BuGate{});
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gn;
       } else {
@@ -263,7 +263,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                                  fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                  anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
                                  next_wide, slabF<W>(rows), nullptr, nullptr, 0, nullptr, nullptr,
-                                 snap);
+                                 snap, BuGate{});
         if (FUSE) rows += gn;
       }
     }
@@ -336,9 +336,130 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   return rows;
 }
 
-#define MSBFS_BP_INST(WW)                                              \
-  template int BitparSolver::level_bu<WW, false>(Loop&, hipStream_t); \
-  template int BitparSolver::level_bu<WW, true>(Loop&, hipStream_t);
+// Pull levels that bu_batch may run: the third pull level on (lists split at kWideLater, every
+// row pulled without probes, no lean pass), active lists of at most tun_.bu_max vertices, no
+// forced directions and no edge counting (k_count_frontier needs per-level host sizes).
+template <int W, bool COUNT>
+bool BitparSolver::bu_batch_ok(const Loop& S) const {
+  // (fsrc_acc: a push level came last; level_bu first clears the accumulator entries of its
+  // frontier, which later pulls and the next batch expect all-zero)
+  if (COUNT || tun_.bu_max <= 0 || tun_.batch <= 1 || !S.have_active || S.bu_levels < 2 ||
+      S.old_stale || S.fsrc_acc || S.na > tun_.bu_max || !S.plan.empty() || tun_.dirs.size() > S.level)
+    return false;
+  if ((double)S.ev < kFilterFrac * (double)g_.nnz) return false;  // level_bu would filter
+  if (tun_.lean && !S.lean_off && S.nact >= tun_.lean_min) return false;
+  return S.stop_level == 0xFFFFFFFFu || S.level + 2 <= S.stop_level;
+}
+
+// A batch of up to bu_next_ pull levels with no host synchronisation (the late levels of
+// scale-free graphs: RMAT levels 4+ cost ~10-50 us of GPU time each, less than a host round
+// trip). Level i reads counter slot i (slot 0 seeded from the host) and writes slot i + 1; its
+// kernels run only while the BuGate on slot i is open (frontier non-empty and the pull -> push
+// test still says pull), so the levels after the frontier dies or the direction turns are
+// no-ops and the host loop resumes exactly where the host-driven levels would be. Both lists
+// (narrow, wide) go through the short-first-step narrow kernel (late levels: most vertices are
+// covered by their first neighbour); the list lengths come from the slots.
+template <int W, bool COUNT>
+void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
+  static_assert(!COUNT, "edge counting keeps host-driven pull levels (bu_batch_ok)");
+  using L = Lay<W>;
+  const Small sm = small();
+  int K = std::max(2, std::min({bu_next_, tun_.batch, kBatch}));
+  if (S.stop_level != 0xFFFFFFFFu) K = (int)std::min<int64_t>(K, (int64_t)S.stop_level - S.level);
+  Ctr* slots = bctr_.as<Ctr>();
+  uint64_t* aslot = (uint64_t*)(slots + kBatch + 1);
+  MSBFS_HIP_CHECK(hipMemsetAsync(bctr_.p, 0, bctr_.bytes, s));
+  k_bu_seed<<<1, 64, 0, s>>>(slots, (uint32_t)S.nf, (unsigned long long)S.ef, (uint32_t)S.nact,
+                             (uint32_t)S.nactw, (unsigned long long)S.ea, sm.alive[S.alv], aslot);
+  MSBFS_HIP_CHECK(hipGetLastError());
+  // lists only shrink: a vertex stays active at most, and keeps its side of the kWideLater split
+  const int gn = grid_for(S.nact + S.nactw, L::TILE, kMaxGrid);
+  const int gw = S.nactw ? grid_for(S.nactw, L::TILE, kMaxGrid) : 0;
+  const int rows = gn + gw, rg = std::max(1, std::min(64, rows / 32));
+  const int next_wide = std::max(opt.wide_degree, kWideLater);
+  const double alpha = alpha_eff();
+  const uint32_t level0 = S.level;
+  const auto t0 = std::chrono::steady_clock::now();
+  trace::Range range_batch("bitpar L%u-%u BU batch", level0 + 1, level0 + K);
+  auto kn = k_bu_narrow<W, false, kBlock, 0, true, false, false, 8, 1>;
+  for (int i = 0; i < K; ++i) {
+    const BuGate gate{slots + i, opt.beta, alpha, i == 0 ? 1 : 0};
+    const int p = i & 1;
+    const uint64_t* R = vis_[S.cur ^ p].as<uint64_t>();
+    uint64_t* O = vis_[S.cur ^ p ^ 1].as<uint64_t>();
+    int32_t* fl_out = fl_[S.fc ^ p ^ 1].as<int32_t>();
+    const uint64_t* alive = aslot + 16 * i;
+    kn<<<gn, kBlock, 0, s>>>(act_[p].as<int32_t>(), 0, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+                             done_.as<uint32_t>(), act_[p ^ 1].as<int32_t>(), fl_out, slots + i + 1,
+                             anyvis_.as<uint32_t>(), INT32_MAX, actw_[p ^ 1].as<int32_t>(),
+                             next_wide, slabF<W>(0), nullptr, nullptr, 0, nullptr,
+                             &slots[i].act2.v, nullptr, gate);
+    if (gw)
+      kn<<<gw, kBlock, 0, s>>>(actw_[p].as<int32_t>(), 0, g_.rowptr, g_.col, R, O, alive,
+                               sm.gmask, done_.as<uint32_t>(), act_[p ^ 1].as<int32_t>(), fl_out,
+                               slots + i + 1, anyvis_.as<uint32_t>(), INT32_MAX,
+                               actw_[p ^ 1].as<int32_t>(), next_wide, slabF<W>(gn), nullptr,
+                               nullptr, 0, nullptr, &slots[i].actw2.v, nullptr, gate);
+    k_level_reduce<W, false><<<W * rg, kBlock, 0, s>>>(slabF<W>(0), slabE<W>(0), rows, rg, sm.F,
+                                                       sm.E, aslot + 16 * (i + 1), level0 + 1 + i,
+                                                       gate);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  MSBFS_HIP_CHECK(hipMemcpyAsync(hbctr_->p, bctr_.p, (size_t)(K + 1) * sizeof(Ctr),
+                                 hipMemcpyDeviceToHost, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  const Ctr* h = hbctr_->as<Ctr>();
+  int real = 0;  // levels whose gate was open (the same test the kernels made)
+  while (real < K && bu_gate_eval(h[real], opt.beta, alpha, real == 0 ? 1 : 0)) {
+    S.ev += (int64_t)h[real + 1].ev2.v;
+    ++real;
+  }
+  MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[S.alv], aslot + 16 * real, 16 * sizeof(uint64_t),
+                                 hipMemcpyDeviceToDevice, s));
+  if (st && real > 0) {  // per-level records; the batch's wall time is split evenly
+    const double ms = std::chrono::duration<double, std::milli>(
+                          std::chrono::steady_clock::now() - t0).count() / real;
+    for (int i = 0; i < real; ++i) {
+      LevelRec rec;
+      rec.batch = (int32_t)st->batches;
+      rec.level = (int32_t)(level0 + 1 + i);
+      rec.dir = 'B';
+      rec.nf = h[i].fl2.v;
+      rec.ef = (int64_t)h[i].ef2.v;
+      rec.nf_next = h[i + 1].fl2.v;
+      rec.active = (int64_t)h[i + 1].act2.v + h[i + 1].actw2.v;  // (as levels(): the new lists)
+      rec.ms = ms;
+      st->recs.push_back(rec);
+    }
+    st->bu_levels += real;
+    st->levels += real;
+  }
+  S.level = level0 + real;
+  S.bu_levels += real;
+  S.nf = h[real].fl2.v;
+  S.ef = (int64_t)h[real].ef2.v;
+  S.nact = h[real].act2.v;
+  S.nactw = h[real].actw2.v;
+  S.na = S.nact + S.nactw;
+  S.ea = (int64_t)h[real].eu2.v;
+  if (real & 1) {  // level i read list / row / frontier buffers of parity i
+    std::swap(act_[0], act_[1]);
+    std::swap(actw_[0], actw_[1]);
+    S.cur ^= 1;
+    S.fc ^= 1;
+  }
+  S.fsrc_acc = false;
+  S.osnap_next = false;
+  // the next batch: twice as long while the frontier lives, else this tail's length + 1
+  bu_next_ = real == K ? std::min(2 * K, kBatch) : real + 1;
+}
+
+#define MSBFS_BP_INST(WW)                                                 \
+  template int BitparSolver::level_bu<WW, false>(Loop&, hipStream_t);    \
+  template int BitparSolver::level_bu<WW, true>(Loop&, hipStream_t);     \
+  template bool BitparSolver::bu_batch_ok<WW, false>(const Loop&) const; \
+  template bool BitparSolver::bu_batch_ok<WW, true>(const Loop&) const;  \
+  template void BitparSolver::bu_batch<WW, false>(Loop&, RunStats*, hipStream_t);
 MSBFS_BP_FOR_W(MSBFS_BP_INST)
 #undef MSBFS_BP_INST
 

@@ -190,7 +190,7 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
           slabF_.as<uint32_t>(), slabE_.as<unsigned long long>());
     k_level_reduce<W, COUNT><<<W * rg, kBlock, 0, s>>>(slabF_.as<uint32_t>(),
                                                        slabE_.as<unsigned long long>(), grid, rg,
-                                                       sm.F, sm.E, aslot + 16 * (i + 1), weight);
+                                                       sm.F, sm.E, aslot + 16 * (i + 1), weight, BuGate{});
     MSBFS_HIP_CHECK(hipGetLastError());
     aidx = i + 1;
     S.fc ^= 1;

@@ -33,19 +33,21 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "code_deg") code_deg = to_num(key, v);
   else if (key == "lean") lean = (int)to_num(key, v);
   else if (key == "lean_min") lean_min = (int64_t)to_num(key, v);
+  else if (key == "lean_level") lean_level = (int)to_num(key, v);
   else if (key == "lazy") lazy = (int)to_num(key, v);
   else if (key == "td_fused") td_fused = (int)to_num(key, v);
   else if (key == "td_bm") td_bm = (int64_t)to_num(key, v);
   else if (key == "batch") {
     batch = (int)to_num(key, v);
     if (batch < 1 || batch > 64) fail("tuning: batch must be in [1, 64]");
-  } else if (key == "dirs") {
+  } else if (key == "bu_max") bu_max = (int64_t)to_num(key, v);
+  else if (key == "dirs") {
     for (char c : v)
       if (c != 'T' && c != 'B' && c != '.') fail("tuning: dirs takes T, B or . per level");
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lazy td_fused td_bm batch dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max dirs)");
   }
 }
 
@@ -244,7 +246,8 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       bottom_up = (double)S.ef > (double)S.ea / alpha_eff() ||
                   (tun_.gamma > 0 && S.level >= 1 &&
                    (double)S.ef > gamma_for(S.level) * (double)n_eff());
-    else bottom_up = !((double)S.nf < (double)S.na / opt.beta && (double)S.ef < (double)S.ea / alpha_eff());
+    else bottom_up = keep_pulling((double)S.nf, (double)S.ef, (double)S.na, (double)S.ea, opt.beta,
+                                  alpha_eff());
     const std::string& dirs = tun_.dirs;
     if (S.level < dirs.size() && (dirs[S.level] == 'T' || dirs[S.level] == 'B'))
       bottom_up = dirs[S.level] == 'B';
@@ -259,6 +262,14 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       tl = std::chrono::steady_clock::now();
       continue;
     }
+    // late pull levels (small active lists: host round trips cost more than the level itself)
+    if constexpr (!COUNT) {
+      if (bottom_up && !trace && bu_batch_ok<W, COUNT>(S)) {
+        bu_batch<W, COUNT>(S, st, s);
+        tl = std::chrono::steady_clock::now();
+        continue;
+      }
+    }
     MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
     MSBFS_HIP_CHECK(hipMemsetAsync(sm.alive[S.alv ^ 1], 0, 16 * sizeof(uint64_t), s));
     ++S.level;
@@ -270,7 +281,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       const int rg = std::max(1, std::min(64, rows / 32));
       const uint32_t weight = (S.level == 1 && !S.weight_l1) ? 0u : S.level;
       k_level_reduce<W, COUNT><<<W * rg, kBlock, 0, s>>>(slabF<W>(0), slabE<W>(0), rows, rg, sm.F,
-                                                         sm.E, sm.alive[S.alv ^ 1], weight);
+                                                         sm.E, sm.alive[S.alv ^ 1], weight, BuGate{});
       MSBFS_HIP_CHECK(hipGetLastError());
     }
     c = read_ctr(s);

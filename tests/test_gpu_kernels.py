@@ -264,12 +264,13 @@ def test_bitpar_forced_direction_plans(msbfs_pkg, dirs):
     for dev, host, K in cases:
         qs = m.QuerySet.random(host.n, K, 4, seed=K)
         ref = m.cpu_bfs(host, qs)
-        with m.Solver(dev, "bitpar", max_groups=min(K, 1024),
-                      tuning={"dirs": dirs} if dirs else None) as s:
-            r = s.run(qs)
-            r2 = s.run(qs)
-        assert np.array_equal(r.F, ref.F), (dirs, K)
-        assert np.array_equal(r2.F, ref.F), (dirs, K)
+        for bu_max in (0, 1 << 30):  # host-driven / device-driven late pull levels
+            tun = {"dirs": dirs, "bu_max": bu_max} if dirs else {"bu_max": bu_max}
+            with m.Solver(dev, "bitpar", max_groups=min(K, 1024), tuning=tun) as s:
+                r = s.run(qs)
+                r2 = s.run(qs)
+            assert np.array_equal(r.F, ref.F), (dirs, K, bu_max)
+            assert np.array_equal(r2.F, ref.F), (dirs, K, bu_max)
 
 
 @pytest.mark.parametrize("knobs", [{"lean_min": 0}, {"lean": 0}, {"lazy": 0},
@@ -293,6 +294,43 @@ def test_bitpar_lean_and_lazy_paths(msbfs_pkg, knobs):
             r2 = s.run(qs)
         assert np.array_equal(r.F, ref.F), (knobs, K)
         assert np.array_equal(r2.F, ref.F), (knobs, K)
+
+
+@pytest.mark.parametrize("tun", [{"bu_max": 1 << 30}, {"bu_max": 1 << 30, "batch": 2},
+                                 {"bu_max": 1 << 30, "batch": 3, "lean": 0}])
+def test_bitpar_device_pull_batches(msbfs_pkg, tun):
+    """Late pull levels as device-driven batches (bu_batch: counter slots, BuGate per level,
+    no-op levels after the frontier dies or the direction turns): answers equal the CPU oracle
+    and the per-level records (level, direction, frontier size and degree sum, next frontier,
+    new active lists) equal the host-driven levels' (tuning bu_max=0), so the device gate took
+    every decision the host loop takes. Short batches (batch=2, 3) chain several per run; the
+    uniform graph turns back to push within a batch; reused solvers; W = 1, 2, 16."""
+    m = msbfs_pkg
+    dg = m.DeviceGraph.rmat(15, 16, 7, device=0)
+    hg = dg.download()
+    cases = [(dg, hg)]
+    rl = m.DeviceGraph.rmat(14, 16, 3, device=0)
+    rh = rl.download()  # (original ids: the queries are mapped on the device)
+    rl.relabel_by_degree()
+    cases.append((rl, rh))
+    u = m.Graph.uniform(30000, 300000, 9)
+    cases.append((u.to_device(0), u))
+    batched = 0
+    for gi, (dev, host) in enumerate(cases):
+        for K in (64, 100, 1024):
+            qs = m.QuerySet.random(host.n, K, 6, seed=K + gi)
+            ref = m.cpu_bfs(host, qs)
+            recs = {}
+            for name, t in (("dev", tun), ("host", {"bu_max": 0})):
+                with m.Solver(dev, "bitpar", max_groups=K, tuning=t) as s:
+                    r = s.run(qs)
+                    assert np.array_equal(r.F, ref.F), (gi, K, name)
+                    assert np.array_equal(s.run(qs).F, ref.F), (gi, K, name)
+                    recs[name] = [(x["batch"], x["level"], x["dir"], x["nf"], x["ef"],
+                                   x["nf_next"], x["active"]) for x in s.level_trace()]
+            assert recs["dev"] == recs["host"], (gi, K)
+            batched += sum(x[2] == "B" and x[1] >= 4 for x in recs["dev"])
+    assert batched > 0
 
 
 def _hyp_strategy():
