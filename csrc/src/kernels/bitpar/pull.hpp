@@ -231,6 +231,9 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
   static_assert(!(FUSE && COUNT), "the edge-counting pass uses k_count_frontier");
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
+  // done / any-visited bits: one atomic per word of the wave (wave_set_bits) where a wave
+  // holds many vertices or many first visits (W = 16 levels 3-4 measured ~0.4 ms slower each)
+  constexpr bool kCombine = G <= 4 || PFX;
   constexpr int NWV = BT / 64, TILE = NWV * VPW;
   constexpr int C = CS;                      // neighbours per step
   constexpr int Q = C / G > 0 ? C / G : 1;   // ids loaded per lane per step
@@ -416,16 +419,14 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
     const bool g_new = (bn >> (sub * G)) & L::GBITS;
     const bool g_nf = (bf >> (sub * G)) & L::GBITS;
     const bool leader = valid && slot == 0;
-    if (leader && !g_nf) set_done(done, v);
+    wave_set_bits<kCombine>(done, v, leader && !g_nf);
     const bool keep = leader && g_nf, app = leader && g_new;
     if (keep) eu += deg;
     if (app) ef += deg;
     {
       const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
-      if (leader && g_first) {
-        atomicOr(&anyvis[v >> 5], 1u << (v & 31));
-        ev += deg;
-      }
+      wave_set_bits<kCombine>(anyvis, v, leader && g_first);
+      if (leader && g_first) ev += deg;
     }
     // third stage: the next tile's first-step ids (its offsets arrived during this tile)
 #pragma unroll
@@ -471,6 +472,9 @@ __global__ __launch_bounds__(kBlock, 8) void k_bu_first(
     int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF, const int32_t* first) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  // done / any-visited bits: one atomic per word of the wave (wave_set_bits) where a wave
+  // holds many vertices or many first visits (W = 16 levels 3-4 measured ~0.4 ms slower each)
+  constexpr bool kCombine = G <= 4;
   constexpr int CR = 65;  // bank-skewed counter rows (see BitCounter::spill_strided)
   __shared__ LdsQueue qo, qf;
   __shared__ unsigned long long scratch[kWaves];
@@ -529,12 +533,10 @@ __global__ __launch_bounds__(kBlock, 8) void k_bu_first(
     const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
     const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
     const bool leader = valid && slot == 0;
-    if (leader && fin) set_done(done, v);
+    wave_set_bits<kCombine>(done, v, leader && fin);
     if (leader && g_new) ef += deg;
-    if (leader && g_first) {
-      atomicOr(&anyvis[v >> 5], 1u << (v & 31));
-      ev += deg;
-    }
+    wave_set_bits<kCombine>(anyvis, v, leader && g_first);
+    if (leader && g_first) ev += deg;
     q_push(qo, leader && !fin, v);
     q_push(qf, leader && g_new, v);
     q_flush(qo, ovf, &ctr->touched.v, TILE, false);
@@ -865,6 +867,9 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const uint32_t* snap) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  // done / any-visited bits: one atomic per word of the wave (wave_set_bits) where a wave
+  // holds many vertices or many first visits (W = 16 levels 3-4 measured ~0.4 ms slower each)
+  constexpr bool kCombine = G <= 4;
   __shared__ LdsQueue qa, qf, qn;
   __shared__ unsigned long long scratch[kWaves];
   // bank-skewed counter rows (see BitCounter::spill_strided): wide vertices gain many groups
@@ -923,16 +928,14 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const bool g_new = (bn >> (sub * G)) & L::GBITS;
     const bool g_nf = (bf >> (sub * G)) & L::GBITS;
     const bool leader = valid && slot == 0;
-    if (leader && !g_nf) set_done(done, v);
+    wave_set_bits<kCombine>(done, v, leader && !g_nf);
     const bool keep = leader && g_nf, app = leader && g_new;
     if (keep) eu += deg;
     if (app) ef += deg;
     {
       const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
-      if (leader && g_first) {
-        atomicOr(&anyvis[v >> 5], 1u << (v & 31));
-        ev += deg;
-      }
+      wave_set_bits<kCombine>(anyvis, v, leader && g_first);
+      if (leader && g_first) ev += deg;
     }
     q_push(qa, keep && (int)deg > next_wide, v);
     q_push(qn, keep && (int)deg <= next_wide, v);
