@@ -122,7 +122,7 @@ __global__ __launch_bounds__(kBlock) void k_build_codes(const uint64_t* R, const
 // first id with degree < 2^k for k = 0..kDegBounds-1 (rows relabelled by descending degree: one
 // binary search per k, one thread each)
 constexpr int kDegBounds = 41;
-__global__ void k_degree_bounds(const int64_t* rowptr, int64_t n, int32_t* out) {
+static __global__ void k_degree_bounds(const int64_t* rowptr, int64_t n, int32_t* out) {
   const int k = threadIdx.x;
   if (k >= kDegBounds) return;
   const int64_t min_deg = (int64_t)1 << k;
@@ -136,7 +136,7 @@ __global__ void k_degree_bounds(const int64_t* rowptr, int64_t n, int32_t* out) 
 }
 
 // number of vertices with degree > d (bounds the wide list of any pull level)
-__global__ __launch_bounds__(kBlock) void k_count_wide(const int64_t* rowptr, int64_t n, int64_t d,
+static __global__ __launch_bounds__(kBlock) void k_count_wide(const int64_t* rowptr, int64_t n, int64_t d,
                                                        unsigned long long* out) {
   __shared__ unsigned long long scratch[kWaves];
   unsigned long long c = 0;
@@ -767,7 +767,7 @@ __device__ __forceinline__ int64_t row_lower_bound(const int32_t* col, int64_t b
 
 // plen[v] = length of v's row prefix with ids < H (rows sorted; a graph property, computed once
 // per graph and bound H, see BitparSolver::prefix_lens)
-__global__ __launch_bounds__(kBlock) void k_prefix_lens(const int64_t* rowptr, const int32_t* col,
+static __global__ __launch_bounds__(kBlock) void k_prefix_lens(const int64_t* rowptr, const int32_t* col,
                                                         int64_t n, int32_t H, int32_t* plen) {
   for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n;
        v += (int64_t)gridDim.x * kBlock) {
@@ -779,7 +779,7 @@ __global__ __launch_bounds__(kBlock) void k_prefix_lens(const int64_t* rowptr, c
 // first[v] = v's first neighbour (rows sorted: after degree relabelling its biggest hub), -1 for
 // an isolated vertex: the lean first-row pass (k_bu_first) reads it with one coalesced 4-byte load
 // instead of the rowptr -> col chain, whose col[rowptr[v]] touches one 128-byte line per vertex
-__global__ __launch_bounds__(kBlock) void k_first_nbr(const int64_t* rowptr, const int32_t* col,
+static __global__ __launch_bounds__(kBlock) void k_first_nbr(const int64_t* rowptr, const int32_t* col,
                                                       int64_t n, int32_t* first) {
   for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n;
        v += (int64_t)gridDim.x * kBlock) {
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(kBlock) void k_first_nbr(const int64_t* rowptr, con
 }
 
 // chunk counts of the wide vertices' row prefixes (inclusive-scanned into offs by the host)
-__global__ __launch_bounds__(kBlock) void k_prefix_chunks(const int32_t* wl, int64_t nw,
+static __global__ __launch_bounds__(kBlock) void k_prefix_chunks(const int32_t* wl, int64_t nw,
                                                           const int32_t* plen, int64_t* cnt) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
        i += (int64_t)gridDim.x * kBlock)
@@ -797,7 +797,7 @@ __global__ __launch_bounds__(kBlock) void k_prefix_chunks(const int32_t* wl, int
 }
 
 // plen != nullptr: chunks cover only the row prefixes with ids < H (prefix-pull level)
-__global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl, int64_t nw,
+static __global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl, int64_t nw,
                                                        const int64_t* offs, const int64_t* rowptr,
                                                        const int32_t* plen, ChunkDesc* desc) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
@@ -858,13 +858,30 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
   }
 }
 
+// 32-bit block sum, one atomic per block
+__device__ __forceinline__ void block_sum_add32(uint32_t val, uint32_t* dst, uint32_t* scratch) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
+  __syncthreads();
+  if (lane_id() == 0) scratch[threadIdx.x >> 6] = val;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += scratch[w];
+    if (t) atomicAdd(dst, t);
+  }
+}
+
 // bottom-up, wide vertices, phase 2: G lanes per vertex fold acc[v] into the visited words.
 template <int W, bool COUNT, bool FUSE>
 __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, uint64_t* Wb,
     uint64_t* acc, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* actw2,
     int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* act2n, int next_wide, uint32_t* slabF,
-    const uint32_t* snap) {
+    const uint32_t* snap, uint32_t* fbm = nullptr) {
+  // fbm != nullptr (the tiled first pull level, see tiles.hpp): wl is the static big-vertex list,
+  // so done vertices are skipped; no list queues: the new frontier goes into bitmap fbm and its
+  // size into ctr->fl2, the next active lists come from k_build_active after the level
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   // done / any-visited bits: one atomic per word of the wave (wave_set_bits) where a wave
@@ -891,15 +908,20 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long eu = 0, ef = 0, ev = 0;
+  uint32_t nfc = 0;
+  __shared__ uint32_t scratch32[kWaves];
   for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nw; tb += (int64_t)gridDim.x * TILE) {
     const int64_t idx = tb + wv * VPW + sub;
-    const bool valid = idx < nw;
+    bool valid = idx < nw;
     int32_t v = 0;
     V<VW> nwb = vzero<VW>();
     bool anynew = false, notfull = false, rnz = false;
     uint32_t deg = 0;
     if (valid) {
       v = wl[idx];
+      if (fbm && is_done(done, v)) valid = false;
+    }
+    if (valid) {
       const int64_t vo = (int64_t)v * W + slot * VW;
       const V<VW> r = (snap && !any_visited(snap, v)) ? vzero<VW>() : ldv<VW>(R + vo);
       const V<VW> a = ldv<VW>(acc + vo);
@@ -930,12 +952,17 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const bool leader = valid && slot == 0;
     wave_set_bits<kCombine>(done, v, leader && !g_nf);
     const bool keep = leader && g_nf, app = leader && g_new;
-    if (keep) eu += deg;
+    if (keep && !fbm) eu += deg;
     if (app) ef += deg;
     {
       const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
       wave_set_bits<kCombine>(anyvis, v, leader && g_first);
       if (leader && g_first) ev += deg;
+    }
+    if (fbm) {  // (uniform)
+      wave_set_bits<kCombine>(fbm, v, app);
+      nfc += app ? 1u : 0u;
+      continue;
     }
     q_push(qa, keep && (int)deg > next_wide, v);
     q_push(qn, keep && (int)deg <= next_wide, v);
@@ -947,6 +974,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
   q_flush(qa, actw2, &ctr->actw2.v, 0, true);
   q_flush(qn, act2n, &ctr->act2.v, 0, true);
   q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  if (fbm) block_sum_add32(nfc, &ctr->fl2.v, scratch32);
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
@@ -960,7 +988,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
 
 // counter slot 0 and alive mask 0 of a device-driven pull batch (bu_batch): the host's view
 // after the level before the batch
-__global__ void k_bu_seed(Ctr* c0, uint32_t nf, unsigned long long ef, uint32_t nact,
+static __global__ void k_bu_seed(Ctr* c0, uint32_t nf, unsigned long long ef, uint32_t nact,
                           uint32_t nactw, unsigned long long eu, const uint64_t* alive,
                           uint64_t* alive0) {
   if (threadIdx.x == 0) {

@@ -76,6 +76,7 @@ struct Tuning {
   // pull levels from the third on run as device-driven batches (bu_batch) while the active lists
   // hold at most bu_max vertices (0 = host-driven pull levels; needs batch > 1)
   int64_t bu_max = 1 << 20;
+  int tiles = 1;       // first pull level over static vertex tiles (bitpar/tiles.hpp)
   std::string dirs;    // forced per-level directions 'T'/'B' (tests, experiments)
 
   void set(const std::string& key, const std::string& value);
@@ -129,6 +130,7 @@ class BitparSolver final : public Solver {
     bool lean_off = false;              // a lean first-row pass overflowed (see k_bu_first)
     bool lean_ran = false;              // this level ran one (its overflow count is c.touched)
     bool old_stale = false;             // k_td_fused levels updated only vis_[cur]
+    bool fl_bitmap = false;             // fl_[fc] not built yet: the frontier is in fbm_tile_
   };
   struct Small {
     unsigned long long* F;
@@ -178,6 +180,21 @@ class BitparSolver final : public Solver {
   template <int W, bool COUNT>
   void bu_batch(Loop& S, RunStats* st, hipStream_t s);
   const int32_t* prefix_lens(int32_t H, hipStream_t s);
+  // ---- bitpar_tiles.hip: the first pull level's prefix pull over static vertex tiles
+  struct TileSet {
+    DevBuf pent, tiles, big;
+    int64_t ntiles = 0, nbig = 0, nent = 0;
+    int part = -1, nparts = 0;
+    const void* key[2] = {nullptr, nullptr};
+  };
+  // the tiles of the own vertices (part of nparts; built on first use and cached per graph
+  // buffers; nullptr for fewer than 8 words or when they do not fit in HBM)
+  const TileSet* pfx_tiles(int W, int part, int nparts, hipStream_t s);
+  template <int W>
+  int tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t* O, const uint32_t* snap,
+                 const uint32_t* codes, int32_t code_from, int rows);
+  // the frontier list of a tiled level is only a bitmap until a top-down level needs it
+  void materialize_frontier(Loop& S, hipStream_t s);
   const int32_t* first_nbr(hipStream_t s);
   int32_t code_bound(double min_deg);
   // ---- bitpar_hybrid.hip
@@ -282,6 +299,10 @@ class BitparSolver final : public Solver {
   const void* code_key_[2] = {nullptr, nullptr};
   int batch_next_ = 4;  // levels of the next device-driven batch (doubles while the frontier lives)
   int bu_next_ = 4;     // levels of the next device-driven pull batch (the last run's pull tail + 1)
+  TileSet tiles_;
+  bool tiles_ok_ = true;  // false once the tiles did not fit
+  DevBuf fbm_tile_, lcnt_;  // frontier bitmap of a tiled level, list counter
+  int num_cus_ = 0;
   DevBuf bctr_;  // (kBatch+1) Ctr slots, then (kBatch+1) x 16 alive words
   std::unique_ptr<PinnedBuf> hbctr_;
 };

@@ -1,0 +1,300 @@
+// Bit-parallel MS-BFS: the first bottom-up level's prefix pull as an edge-streaming kernel over
+// static vertex tiles (k_pfx_tiles), replacing the narrow lane-group pull and the hub chunks on
+// that level.
+//
+// Why: the per-vertex pulls (k_bu_narrow, one lane group per vertex, 4-8 neighbours per step and
+// a coverage ballot between steps) chain their loads (list entry -> offsets -> column ids ->
+// probe -> rows) and sync the block for their list queues every tile; on RMAT-26 / 1024 groups
+// the level-2 pulls run at about half the rate the chip gathers rows and codes at
+// (profiles/gather_rates.md). The first pull level never exits early (hardly any vertex gets all
+// its groups at level 2), so its work is a plain boolean SpMM over the row prefixes:
+//     Y[v] = OR_{u in prefix(v), u visited} row(u)
+// and can be streamed edge by edge with no per-vertex loop.
+//
+// Layout (built once per graph, prefix bound H and vertex partition; BitparSolver::pfx_tiles):
+//   pent[] = every own vertex's prefix column ids (ids < H <= 2^19) in vertex order, packed as
+//            u | vl << 19 with vl = the vertex's index inside its tile (< VT)
+//   tiles  = consecutive own vertices (<= VT of them, ~kTileWeight entries + kVertexWeight per
+//            vertex) with their entry range; a vertex with more than kBigPrefix entries gets
+//            partial tiles of its own (kPartialEntries each) instead, whose results are OR-ed
+//            into acc[v] and folded in by k_bu_wide_finalize over the big-vertex list.
+// One wave per tile, no block barriers: entries are loaded 256 at a time (4 per lane,
+// coalesced), probed against the LDS hub bitmap, single-group codes OR their bits into the
+// wave's LDS accumulator rows, the rest are compacted and their rows gathered by lane groups
+// (several rows in flight per group) and OR-ed into the accumulator rows. The epilogue is the
+// narrow pull's (new bits, row store, counters, done / any-visited bits) minus the list
+// queues: the frontier goes into a bitmap (materialised as a list only if a top-down level
+// follows) and the next active lists come from one k_build_active pass after the level.
+#pragma once
+
+#include "common.hpp"
+#include "pull.hpp"
+
+namespace msbfs {
+namespace bp {
+
+struct PfxTile {
+  int32_t v0;   // first vertex
+  int32_t nv;   // vertices (low 16 bits); kTilePartial: one vertex, a slice of its entries
+  int64_t e0;   // first entry in pent (the next tile's e0 ends it)
+};
+constexpr int32_t kTilePartial = 1 << 16;
+constexpr uint32_t kPentNone = 0xFFFFFFFFu;
+constexpr int kPentUBits = 19;                     // u < 2^19 (H = 458752)
+constexpr uint32_t kPentUMask = (1u << kPentUBits) - 1;
+constexpr int kTileWeight = 1024;   // entries + kVertexWeight * vertices per tile (target)
+constexpr int kBigPrefix = 1024;    // more prefix entries: partial tiles
+constexpr int kPartialEntries = 1024;
+constexpr int kTileBlock = 1024;    // one block per CU: the hub bitmap + 16 waves' rows
+constexpr int kTileHubW = 14336;    // hub bitmap words (ids < 458752, the prefix bound)
+
+// vertices per tile (the wave's accumulator rows: VT x W words, 4 KB at W = 16; the same tiles
+// serve every word count) and the weight of a vertex besides its entries
+constexpr int kTileVT = 32;
+constexpr int kVertexWeight = kTileWeight / kTileVT;
+
+// pent for the vertices of normal tiles (one wave per tile: a wave prefix sum over the <= VT
+// prefix lengths) and of the big vertices (one wave per vertex, vl = 0)
+__global__ __launch_bounds__(256) void k_fill_pent(const PfxTile* tiles, int64_t ntiles,
+                                                   int nparts, const int64_t* rowptr,
+                                                   const int32_t* col, const int32_t* plen,
+                                                   uint32_t* pent) {
+  const int lane = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t t = wave; t < ntiles; t += nw) {
+    const PfxTile d = tiles[t];
+    const int64_t e1 = tiles[t + 1].e0;
+    if (d.nv & kTilePartial) {
+      // slice [k0, k0 + (e1 - e0)) of the vertex's prefix: partial tiles of one vertex are
+      // consecutive, the first one starts at the vertex's first entry
+      int64_t first = t;
+      while (first > 0 && (tiles[first - 1].nv & kTilePartial) && tiles[first - 1].v0 == d.v0)
+        --first;
+      const int64_t k0 = d.e0 - tiles[first].e0;
+      const int64_t b = rowptr[d.v0] + k0;
+      for (int64_t k = lane; k < e1 - d.e0; k += 64) pent[d.e0 + k] = (uint32_t)col[b + k];
+      continue;
+    }
+    const int nv = d.nv & 0xFFFF;
+    int64_t e = d.e0;
+    for (int i = 0; i < nv; ++i) {
+      const int32_t v = d.v0 + i * nparts;
+      const int32_t p = plen[v];
+      const int64_t b = rowptr[v];
+      for (int k = lane; k < p; k += 64) pent[e + k] = (uint32_t)col[b + k] | ((uint32_t)i << kPentUBits);
+      e += p;
+    }
+  }
+}
+
+// PB rows in flight per lane group in the gather step
+template <int W>
+__global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
+    const PfxTile* __restrict__ tiles, int64_t ntiles, const uint32_t* __restrict__ pent,
+    int nparts, const int64_t* rowptr, const uint64_t* R, uint64_t* O, uint64_t* acc,
+    const uint32_t* pvis, const uint32_t* snap, const uint32_t* code, int32_t code_from,
+    const uint64_t* alive, const uint64_t* gmask, uint32_t* done, uint32_t* anyvis, uint32_t* fbm,
+    const int32_t* stamp, int32_t epoch, Ctr* ctr, uint32_t* slabF) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, S = 64 / G, VT = kTileVT;
+  constexpr int NWV = kTileBlock / 64;
+  constexpr int PB = 4;       // rows in flight per lane group
+  constexpr int Q = 4;        // entries per lane per round
+  constexpr int CR = 65;      // bank-skewed counter rows (BitCounter::spill_strided)
+  __shared__ uint32_t hub[kTileHubW];
+  __shared__ unsigned long long Y[NWV][VT * W];
+  __shared__ uint32_t lst[NWV][64 * Q];
+  __shared__ uint32_t cnt[CR * W];
+  __shared__ unsigned long long scratch[NWV];
+  __shared__ uint32_t scratch32[NWV];
+  for (int i = threadIdx.x; i < kTileHubW; i += kTileBlock) hub[i] = pvis[i];
+  for (int i = threadIdx.x; i < CR * W; i += kTileBlock) cnt[i] = 0;
+  __syncthreads();
+  const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
+  unsigned long long* y = Y[wv];
+  uint32_t* ls = lst[wv];
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  unsigned long long ef = 0, ev = 0;
+  uint32_t nfc = 0;
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
+  const int64_t wave = (int64_t)blockIdx.x * NWV + wv;
+  const int64_t nwaves = (int64_t)gridDim.x * NWV;
+  for (int64_t t = wave; t < ntiles; t += nwaves) {
+    const int32_t v0 = uni32(tiles[t].v0);
+    const int32_t nvf = uni32(tiles[t].nv);
+    const int64_t e0 = uni64(tiles[t].e0), e1 = uni64(tiles[t + 1].e0);
+    const int nv = (nvf & kTilePartial) ? 1 : (nvf & 0xFFFF);
+#pragma unroll
+    for (int k = lane; k < VT * W; k += 64) y[k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (int64_t e = e0; e < e1; e += 64 * Q) {
+      uint32_t pk[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int64_t i = e + q * 64 + lane;
+        pk[q] = i < e1 ? pent[i] : kPentNone;
+      }
+      // visited hubs only (the LDS bitmap: any-visited at the level start)
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (pk[q] != kPentNone) {
+          const uint32_t u = pk[q] & kPentUMask;
+          if (!((hub[u >> 5] >> (u & 31)) & 1u)) pk[q] = kPentNone;
+        }
+      // sparse codes: the bits go straight into the accumulator rows
+      uint32_t cd[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        cd[q] = kDenseCode;
+        if (pk[q] != kPentNone && (int32_t)(pk[q] & kPentUMask) >= code_from)
+          cd[q] = code[pk[q] & kPentUMask];
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (pk[q] != kPentNone && cd[q] != kDenseCode) {
+          const int vl = (int)(pk[q] >> kPentUBits);
+#pragma unroll
+          for (int i = 0; i < kCodeSlots; ++i) {
+            const int g = code_g(cd[q], i);
+            if (g >= 0) atomicOr(&y[vl * W + (g >> 6)], 1ull << (g & 63));
+          }
+          pk[q] = kPentNone;
+        }
+      // the rest: dense rows, compacted into the wave's list
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const bool keep = pk[q] != kPentNone;
+        const uint64_t m = __ballot(keep);
+        if (keep) ls[c + __popcll(m & lanemask_lt())] = pk[q];
+        c += __popcll(m);
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (int b = 0; b < c; b += PB * S) {
+        uint32_t uu[PB];
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+          const int k = b + q * S + sub;
+          uu[q] = k < c ? ls[k] : kPentNone;
+        }
+        V<VW> x[PB];
+#pragma unroll
+        for (int q = 0; q < PB; ++q)
+          x[q] = uu[q] != kPentNone
+                     ? ldv<VW>(R + (int64_t)(uu[q] & kPentUMask) * W + slot * VW)
+                     : vzero<VW>();
+#pragma unroll
+        for (int q = 0; q < PB; ++q)
+          if (uu[q] != kPentNone) {
+            const int vl = (int)(uu[q] >> kPentUBits);
+#pragma unroll
+            for (int j = 0; j < VW; ++j)
+              if (x[q].w[j]) atomicOr(&y[vl * W + slot * VW + j], x[q].w[j]);
+          }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (nvf & kTilePartial) {
+      // a slice of a big vertex: publish its bits (k_bu_wide_finalize folds them in)
+      if (sub == 0) {
+        const int64_t vo = (int64_t)v0 * W + slot * VW;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          const uint64_t a = y[slot * VW + j];
+          if (a) atomicOr((unsigned long long*)&acc[vo + j], a);
+        }
+      }
+      continue;
+    }
+    // epilogue: VPW vertices per pass, G lanes each (the narrow pull's, without list queues)
+    for (int p = 0; p < nv; p += VPW) {
+      const int i = p + sub;
+      const int32_t v = v0 + i * nparts;
+      bool valid = i < nv;
+      uint32_t deg = 0;
+      if (valid) {
+        deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
+        valid = deg > 0 && !is_done(done, v);
+      }
+      V<VW> r = vzero<VW>(), a = vzero<VW>();
+      if (valid) {
+        const int64_t vo = (int64_t)v * W + slot * VW;
+        if (!(snap && !any_visited(snap, v))) r = ldv<VW>(R + vo);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) a.w[j] = y[i * W + slot * VW + j];
+        if (stamp[v] == epoch) {  // bits pushed from the tail frontier (k_push_tail)
+          const V<VW> pa = ldv<VW>(acc + vo);
+#pragma unroll
+          for (int j = 0; j < VW; ++j) a.w[j] |= pa.w[j];
+          stv<VW>(acc + vo, vzero<VW>());
+        }
+      }
+      V<VW> nw, nvr;
+      bool anynew = false, notfull = false, rnz = false;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        const uint64_t unv = ~r.w[j] & am.w[j];
+        nw.w[j] = valid ? a.w[j] & unv : 0;
+        nvr.w[j] = r.w[j] | nw.w[j];
+        anynew |= nw.w[j] != 0;
+        notfull |= (unv & ~nw.w[j]) != 0;
+        rnz |= r.w[j] != 0;
+      }
+      if (valid) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
+      bc.add(nw);
+      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+        bc.template spill_strided<CR>(cnt, slot);
+        nadd = 0;
+      }
+      const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
+      const bool g_nf = (__ballot(notfull) >> (sub * G)) & L::GBITS;
+      const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
+      const bool leader = valid && slot == 0;
+      wave_set_bits<true>(done, v, leader && !g_nf);
+      wave_set_bits<true>(fbm, v, leader && g_new);
+      wave_set_bits<true>(anyvis, v, leader && g_first);
+      if (leader && g_new) {
+        ++nfc;
+        ef += deg;
+      }
+      if (leader && g_first) ev += deg;
+    }
+  }
+  block_sum_add32(nfc, &ctr->fl2.v, scratch32);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
+  bc.template spill_strided<CR>(cnt, slot);
+  __syncthreads();
+  uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+  for (int i = threadIdx.x; i < 64 * W; i += kTileBlock) row[i] = cnt[i + (i >> 6)];
+}
+
+// frontier list from the frontier bitmap (LDS block queue; rare: only when a top-down level
+// follows a tiled pull). Block-uniform loops: q_flush synchronises the block.
+__global__ __launch_bounds__(kBlock) void k_bitmap_list(const uint32_t* bm, int64_t nwords,
+                                                        int32_t* out, Ctr* ctr) {
+  __shared__ LdsQueue q;
+  q_init(q);
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t n = (nwords + stride - 1) / stride * stride;
+  for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < n; w += stride) {
+    uint32_t b = w < nwords ? bm[w] : 0u;
+    for (int k = 0; k < 32; ++k) {  // at most one item per thread per step
+      const bool has = b != 0;
+      const int bit = has ? __ffs(b) - 1 : 0;
+      if (has) b &= b - 1;
+      q_push(q, has, (int32_t)(w * 32 + bit));
+      q_flush(q, out, &ctr->touched.v, kBlock, false);
+    }
+  }
+  q_flush(q, out, &ctr->touched.v, 0, true);
+}
+
+}  // namespace bp
+}  // namespace msbfs

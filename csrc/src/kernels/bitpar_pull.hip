@@ -77,7 +77,10 @@ int32_t BitparSolver::code_bound(double min_deg) {
 void BitparSolver::prepare(hipStream_t s) {
   const int64_t ne = n_eff();
   constexpr int32_t kPfxH = 14336 * 32;  // (the prefix pull's bound, see level_bu)
-  if (g_.rows_sorted && g_.n <= INT32_MAX && tun_.pfx == 2) prefix_lens(kPfxH, s);
+  if (g_.rows_sorted && g_.n <= INT32_MAX && tun_.pfx == 2) {
+    prefix_lens(kPfxH, s);
+    if (maxW_ >= 8) (void)pfx_tiles(maxW_, 0, 1, s);  // (the first pull level's tiles)
+  }
   if (tun_.lean) first_nbr(s);
   (void)code_bound(1.0);
   DevBuf c;
@@ -115,7 +118,16 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     S.old_stale = false;
   }
   const int next_wide = std::max(opt.wide_degree, kWideLater);
-  if (!S.have_active) {
+  // the first pull level at level 2 with the prefix pull streams static vertex tiles
+  // (bitpar/tiles.hpp) instead of pulling per vertex from active lists
+  constexpr int kHubW = 14336, kHubBig = 32768;
+  const bool tiled = !COUNT && W >= 8 && tun_.tiles && tun_.pfx == 2 && S.bu_levels == 0 &&
+                     S.level == 2 && g_.rows_sorted && n <= INT32_MAX &&
+                     n > (int64_t)kHubBig * 32 * 4 &&
+                     ((S.lazy && S.bu_levels == 0) || (double)S.ev < kFilterFrac * (double)g_.nnz) &&
+                     pfx_tiles(W, S.part, S.nparts, s) != nullptr;
+  S.fl_bitmap = false;  // this level writes its own frontier (list, or bitmap when tiled)
+  if (!S.have_active && !tiled) {
     // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
     // off only for much higher degrees, so later lists are split at a higher threshold
     const int wide0 = S.bu_levels == 0 ? opt.wide_degree : next_wide;
@@ -157,7 +169,6 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   // probes of the lowest ids (the hubs after degree relabelling) read an LDS copy of their
   // bitmap words: 56 KB (ids < 458752, two blocks per CU) or, where one 1024-thread block per CU
   // has the LDS to itself, 128 KB (ids < 1M)
-  constexpr int kHubW = 14336, kHubBig = 32768;
   const bool hub_lds = filter_from == 0 && n > (int64_t)kHubW * 32 * 4;
   const bool hub_big = n > (int64_t)kHubBig * 32 * 4;
   // counting fused into the traversal kernels (the edge-count pass keeps k_count_frontier)
@@ -197,7 +208,10 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
         stamp_.as<int32_t>(), epoch_);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
-  if (S.nact) {
+  if (tiled) {
+    rows = tiles_pull<W>(S, s, R, O, snap, codes, code_from, rows);
+    S.have_active = S.level < S.stop_level;
+  } else if (S.nact) {
     if (pfx) {
       constexpr int BT = 1024;
       const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
@@ -269,7 +283,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     }
     MSBFS_HIP_CHECK(hipGetLastError());
   }
-  if (S.nactw) {
+  if (S.nactw && !tiled) {
     if (pfx) {  // chunks of the row prefixes with ids < H only
       int64_t* cnt = scan_tmp_.as<int64_t>();
       char* t2 = (char*)scan_tmp_.p + (((size_t)S.nactw * sizeof(int64_t) + 255) & ~size_t(255));
@@ -366,6 +380,7 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
   const Small sm = small();
   int K = std::max(2, std::min({bu_next_, tun_.batch, kBatch}));
   if (S.stop_level != 0xFFFFFFFFu) K = (int)std::min<int64_t>(K, (int64_t)S.stop_level - S.level);
+  S.fl_bitmap = false;  // (the batch's levels write frontier lists)
   Ctr* slots = bctr_.as<Ctr>();
   uint64_t* aslot = (uint64_t*)(slots + kBatch + 1);
   MSBFS_HIP_CHECK(hipMemsetAsync(bctr_.p, 0, bctr_.bytes, s));

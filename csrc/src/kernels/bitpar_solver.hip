@@ -41,13 +41,14 @@ void Tuning::set(const std::string& key, const std::string& v) {
     batch = (int)to_num(key, v);
     if (batch < 1 || batch > 64) fail("tuning: batch must be in [1, 64]");
   } else if (key == "bu_max") bu_max = (int64_t)to_num(key, v);
+  else if (key == "tiles") tiles = (int)to_num(key, v);
   else if (key == "dirs") {
     for (char c : v)
       if (c != 'T' && c != 'B' && c != '.') fail("tuning: dirs takes T, B or . per level");
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles dirs)");
   }
 }
 
@@ -255,6 +256,7 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
       bottom_up = S.plan[S.level] == 'B';
     // low-degree graphs (road-like: thousands of small top-down levels): run a batch of levels
     // without host round trips (kernels read the frontier sizes from device counters)
+    if (!bottom_up) materialize_frontier(S, s);  // (a tiled pull left only its bitmap)
     if (!bottom_up && tun_.batch > 1 && g_.max_degree <= kSmallDeg && !trace &&
         S.level + 2 < S.stop_level && opt.force_dir != 2 && S.plan.empty() &&
         (dirs.size() <= S.level)) {

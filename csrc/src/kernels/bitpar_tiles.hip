@@ -1,0 +1,194 @@
+// Bit-parallel MS-BFS solver: the first pull level's prefix pull over static vertex tiles
+// (kernels and rationale: bitpar/tiles.hpp). Tiles are built once per graph, word count and
+// vertex partition (prepare(), or the first hybrid phase A of a partition), outside any timed
+// run.
+#include <algorithm>
+#include <vector>
+
+#include "bitpar/init.hpp"
+#include "bitpar/solver.hpp"
+#include "bitpar/tiles.hpp"
+
+namespace msbfs {
+namespace bp {
+
+namespace {
+void greedy_tiles(const std::vector<int32_t>& plen, int64_t cnt, int part, int nparts,
+                  std::vector<PfxTile>& tiles, std::vector<int32_t>& big, int64_t& nent) {
+  constexpr int VT = kTileVT, VWT = kVertexWeight;
+  int64_t e = 0;
+  int32_t v0 = 0;
+  int nv = 0;
+  int64_t w = 0, te0 = 0;
+  auto close = [&] {
+    if (nv > 0) tiles.push_back(PfxTile{v0, nv, te0});
+    nv = 0;
+    w = 0;
+  };
+  for (int64_t i = 0; i < cnt; ++i) {
+    const int32_t v = (int32_t)(part + i * nparts);
+    const int64_t p = plen[(size_t)i];
+    if (p > kBigPrefix) {
+      close();
+      big.push_back(v);
+      for (int64_t k = 0; k < p; k += kPartialEntries) {
+        tiles.push_back(PfxTile{v, kTilePartial | 1, e});
+        e += std::min<int64_t>(kPartialEntries, p - k);
+      }
+      continue;
+    }
+    if (nv == VT || (nv > 0 && w + p + VWT > kTileWeight)) close();
+    if (nv == 0) {
+      v0 = v;
+      te0 = e;
+    }
+    ++nv;
+    w += p + VWT;
+    e += p;
+  }
+  close();
+  tiles.push_back(PfxTile{0, 0, e});  // sentinel: ends the last tile
+  nent = e;
+}
+
+__global__ void k_gather_plen(const int32_t* plen, int64_t cnt, int part, int nparts,
+                              int32_t* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = plen[part + i * nparts];
+}
+}  // namespace
+
+const BitparSolver::TileSet* BitparSolver::pfx_tiles(int W, int part, int nparts, hipStream_t s) {
+  if (!tiles_ok_ || !tun_.tiles) return nullptr;
+  TileSet& T = tiles_;
+  if (W < 8) return nullptr;
+  if (T.key[0] == (const void*)g_.rowptr && T.key[1] == (const void*)g_.col &&
+      T.part == part && T.nparts == nparts)
+    return &T;
+  constexpr int32_t kPfxH = kTileHubW * 32;
+  const int32_t* plen = prefix_lens(kPfxH, s);
+  const int64_t ne = n_eff(), cnt = ne > part ? (ne - part + nparts - 1) / nparts : 0;
+  std::vector<int32_t> hp((size_t)std::max<int64_t>(cnt, 1));
+  {
+    DevBuf d((size_t)std::max<int64_t>(cnt, 1) * sizeof(int32_t));
+    if (cnt > 0) {
+      k_gather_plen<<<grid_for(cnt, 256, 8192), 256, 0, s>>>(plen, cnt, part, nparts,
+                                                              d.as<int32_t>());
+      MSBFS_HIP_CHECK(hipGetLastError());
+      MSBFS_HIP_CHECK(hipMemcpyAsync(hp.data(), d.p, (size_t)cnt * sizeof(int32_t),
+                                     hipMemcpyDeviceToHost, s));
+    }
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  std::vector<PfxTile> tl;
+  std::vector<int32_t> big;
+  int64_t nent = 0;
+  greedy_tiles(hp, cnt, part, nparts, tl, big, nent);
+  T.pent.release();
+  T.tiles.release();
+  T.big.release();
+  T.key[0] = T.key[1] = nullptr;
+  const size_t pb = (size_t)std::max<int64_t>(nent, 1) * sizeof(uint32_t);
+  const size_t tb = tl.size() * sizeof(PfxTile), bb = std::max<size_t>(big.size(), 1) * 4;
+  size_t fr = 0, tot = 0;
+  MSBFS_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+  if (pb + tb + bb + ((size_t)4 << 30) > fr) {  // (RMAT-30: keep the per-vertex pulls)
+    tiles_ok_ = false;
+    return nullptr;
+  }
+  T.pent.alloc(pb);
+  T.tiles.alloc(tb);
+  T.big.alloc(bb);
+  MSBFS_HIP_CHECK(hipMemcpyAsync(T.tiles.p, tl.data(), tb, hipMemcpyHostToDevice, s));
+  if (!big.empty())
+    MSBFS_HIP_CHECK(hipMemcpyAsync(T.big.p, big.data(), big.size() * 4, hipMemcpyHostToDevice, s));
+  T.ntiles = (int64_t)tl.size() - 1;
+  T.nbig = (int64_t)big.size();
+  T.nent = nent;
+  if (T.ntiles > 0) {
+    k_fill_pent<<<grid_for(T.ntiles * 64, 256, 16384), 256, 0, s>>>(
+        T.tiles.as<PfxTile>(), T.ntiles, nparts, g_.rowptr, g_.col, plen, T.pent.as<uint32_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));  // (tl / big are host vectors)
+  T.part = part;
+  T.nparts = nparts;
+  T.key[0] = g_.rowptr;
+  T.key[1] = g_.col;
+  if (num_cus_ == 0) {
+    hipDeviceProp_t prop;
+    MSBFS_HIP_CHECK(hipGetDeviceProperties(&prop, g_.device));
+    num_cus_ = prop.multiProcessorCount;
+  }
+  fbm_tile_.ensure((size_t)((g_.n + 31) / 32 + 1) * sizeof(uint32_t));
+  lcnt_.ensure(sizeof(Ctr));
+  return &T;
+}
+
+// The first pull level of a batch over the tiles (see level_bu: called after the tail push).
+// Returns the slab rows it wrote; leaves the next active lists in act_[1] / actw_[1] and the
+// frontier in fbm_tile_ (S.fl_bitmap).
+template <int W>
+int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t* O,
+                             const uint32_t* snap, const uint32_t* codes, int32_t code_from,
+                             int rows) {
+  if constexpr (W < 8) {
+    fail("tiled pull: needs 8 or 16 words");
+  } else {
+  const TileSet* T = pfx_tiles(W, S.part, S.nparts, s);
+  const Small sm = small();
+  const uint64_t* alive = sm.alive[S.alv];
+  const int64_t nwords = (g_.n + 31) / 32;
+  MSBFS_HIP_CHECK(hipMemsetAsync(fbm_tile_.p, 0, (size_t)nwords * sizeof(uint32_t), s));
+  const uint32_t* pvis = snap ? snap : anyvis_.as<uint32_t>();
+  const int grid = std::max(1, num_cus_);
+  k_pfx_tiles<W><<<grid, kTileBlock, 0, s>>>(
+      T->tiles.as<PfxTile>(), T->ntiles, T->pent.as<uint32_t>(), S.nparts, g_.rowptr, R, O,
+      acc_[S.ac].as<uint64_t>(), pvis, snap, codes, codes ? code_from : INT32_MAX, alive,
+      sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), fbm_tile_.as<uint32_t>(),
+      stamp_.as<int32_t>(), epoch_, ctr_.as<Ctr>(), slabF<W>(rows));
+  MSBFS_HIP_CHECK(hipGetLastError());
+  rows += grid;
+  if (T->nbig) {
+    const int gw = grid_for(T->nbig, Lay<W>::TILE, kMaxGrid);
+    k_bu_wide_finalize<W, false, true><<<gw, kBlock, 0, s>>>(
+        T->big.as<int32_t>(), T->nbig, g_.rowptr, R, O, acc_[S.ac].as<uint64_t>(), alive,
+        sm.gmask, done_.as<uint32_t>(), nullptr, nullptr, ctr_.as<Ctr>(),
+        anyvis_.as<uint32_t>(), nullptr, 0, slabF<W>(rows), snap, fbm_tile_.as<uint32_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+    rows += gw;
+  }
+  // next active lists (a hybrid phase A stops here: nothing reads them)
+  if (S.level < S.stop_level) {
+    const int next_wide = std::max(opt.wide_degree, kWideLater);
+    k_build_active<4096><<<grid_for(S.cnt, 4096, INT32_MAX), kBlock, 0, s>>>(
+        S.cnt, S.part, S.nparts, g_.rowptr, done_.as<uint32_t>(), next_wide,
+        act_[1].as<int32_t>(), actw_[1].as<int32_t>(), ctr_.as<Ctr>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+  }
+  S.fl_bitmap = true;
+  }
+  return rows;
+}
+
+// fl_[fc] from the frontier bitmap of a tiled level (only a top-down level reads the list)
+void BitparSolver::materialize_frontier(Loop& S, hipStream_t s) {
+  if (!S.fl_bitmap) return;
+  S.fl_bitmap = false;
+  if (S.nf <= 0) return;
+  const int64_t nwords = (g_.n + 31) / 32;
+  MSBFS_HIP_CHECK(hipMemsetAsync(lcnt_.p, 0, sizeof(Ctr), s));
+  k_bitmap_list<<<grid_for(nwords, kBlock, 2048), kBlock, 0, s>>>(
+      fbm_tile_.as<uint32_t>(), nwords, fl_[S.fc].as<int32_t>(), lcnt_.as<Ctr>());
+  MSBFS_HIP_CHECK(hipGetLastError());
+}
+
+#define MSBFS_BP_INST(WW)                                                                     \
+  template int BitparSolver::tiles_pull<WW>(Loop&, hipStream_t, const uint64_t*, uint64_t*,   \
+                                            const uint32_t*, const uint32_t*, int32_t, int);
+MSBFS_BP_FOR_W(MSBFS_BP_INST)
+#undef MSBFS_BP_INST
+
+}  // namespace bp
+}  // namespace msbfs

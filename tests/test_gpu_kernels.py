@@ -246,6 +246,35 @@ def test_bitpar_prefix_pull_tail_push(msbfs_pkg):
     g.close()
 
 
+@pytest.mark.parametrize("K", [1024, 500])
+def test_bitpar_tiled_first_pull(msbfs_pkg, K):
+    """The first pull level over static vertex tiles (k_pfx_tiles + big-vertex partial tiles +
+    k_bu_wide_finalize, bitpar/tiles.hpp) on a relabelled RMAT-23, 16 and 8 words: identical F
+    with the tiles on and off, with and without sparse codes, with a top-down level right after
+    the tiled one (the frontier list comes from the tile bitmap), and equal to the per-group
+    distance solver on a sample."""
+    m = msbfs_pkg
+    g = m.DeviceGraph.rmat(23, 16, 7, device=0)
+    g.relabel_by_degree()
+    qs = m.QuerySet.random(g.n, K, 16, seed=K)
+    runs = {"tiles": {}, "plain": {"tiles": 0}, "nocodes": {"codes": 0},
+            "td3": {"dirs": "TBT"}, "td3plain": {"dirs": "TBT", "tiles": 0}}
+    out = {}
+    for name, tun in runs.items():
+        with m.Solver(g, "bitpar", max_groups=qs.K, tuning=tun) as s:
+            s.prepare()
+            out[name] = s.run(qs).F
+            out[name + "2"] = s.run(qs).F  # reuse: the acc rows and stamps were left clean
+            tr = s.level_trace()
+        assert "".join(t["dir"] for t in tr).startswith("TBT" if "td3" in name else "TB")
+    for name in out:
+        assert np.array_equal(out[name], out["plain"]), name
+    sub = qs.subset(np.arange(0, K, 97))
+    with m.Solver(g, "dist") as ds:
+        assert np.array_equal(ds.run(sub).F, out["tiles"][::97])
+    g.close()
+
+
 @pytest.mark.parametrize("dirs", ["", "TBBBBBBBBBBBBBBBBBBB", "TBBTBBTBBTBBTBBT", "TBTBTBTBTBTBTBTB",
                                   "TTBBTTBBTTBB"])
 def test_bitpar_forced_direction_plans(msbfs_pkg, dirs):
