@@ -77,6 +77,7 @@ struct Tuning {
   // hold at most bu_max vertices (0 = host-driven pull levels; needs batch > 1)
   int64_t bu_max = 1 << 20;
   int tiles = 1;       // first pull level over static vertex tiles (bitpar/tiles.hpp)
+  int tiles_exp = 0;   // timing experiments in k_pfx_tiles (wrong results; kernel A/B only)
   std::string dirs;    // forced per-level directions 'T'/'B' (tests, experiments)
 
   void set(const std::string& key, const std::string& value);
@@ -188,7 +189,7 @@ class BitparSolver final : public Solver {
     const void* key[2] = {nullptr, nullptr};
   };
   // the tiles of the own vertices (part of nparts; built on first use and cached per graph
-  // buffers; nullptr for fewer than 8 words or when they do not fit in HBM)
+  // buffers; nullptr unless W = 16, or when they do not fit in HBM)
   const TileSet* pfx_tiles(int W, int part, int nparts, hipStream_t s);
   template <int W>
   int tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t* O, const uint32_t* snap,
@@ -299,9 +300,9 @@ class BitparSolver final : public Solver {
   const void* code_key_[2] = {nullptr, nullptr};
   int batch_next_ = 4;  // levels of the next device-driven batch (doubles while the frontier lives)
   int bu_next_ = 4;     // levels of the next device-driven pull batch (the last run's pull tail + 1)
-  TileSet tiles_;
+  std::vector<std::unique_ptr<TileSet>> tilesets_;  // per vertex partition (hybrid emulation: all)
   bool tiles_ok_ = true;  // false once the tiles did not fit
-  DevBuf fbm_tile_, lcnt_;  // frontier bitmap of a tiled level, list counter
+  DevBuf fbm_tile_, lcnt_, zrow_;  // frontier bitmap of a tiled level, list counter, zero row
   int num_cus_ = 0;
   DevBuf bctr_;  // (kBatch+1) Ctr slots, then (kBatch+1) x 16 alive words
   std::unique_ptr<PinnedBuf> hbctr_;

@@ -88,23 +88,64 @@ __global__ __launch_bounds__(256) void k_fill_pent(const PfxTile* tiles, int64_t
   }
 }
 
-// PB rows in flight per lane group in the gather step
+// One round = up to kRound entries of one tile. Rounds are software-pipelined across the
+// wave's tiles (tile t, t + nwaves, ...): while round r is processed, the codes of round r + 1
+// and the packed entries of round r + 2 are in flight, so a round waits for its row gathers
+// only (the entry stream comes from HBM, the codes from L2).
+constexpr int kRoundQ = 4;                 // entries per lane per round
+constexpr int kRound = 64 * kRoundQ;
+struct TileRound {
+  int64_t t, e, e0, e1;  // tile (>= ntiles: none), first entry, the tile's entry range
+};
+__device__ __forceinline__ TileRound tile_first_round(const PfxTile* tiles, int64_t ntiles,
+                                                      int64_t t) {
+  if (t >= ntiles) return TileRound{t, 0, 0, 0};
+  const int64_t e0 = uni64(tiles[t].e0), e1 = uni64(tiles[t + 1].e0);
+  return TileRound{t, e0, e0, e1};
+}
+__device__ __forceinline__ TileRound tile_next_round(const PfxTile* tiles, int64_t ntiles,
+                                                     int64_t nwaves, const TileRound& r) {
+  if (r.t >= ntiles) return r;
+  if (r.e + kRound < r.e1) return TileRound{r.t, r.e + kRound, r.e0, r.e1};
+  return tile_first_round(tiles, ntiles, r.t + nwaves);
+}
+
+// 8 group-uniform ballot bytes (lane group k = bits 8k..8k+7, all set or all clear) -> bit k
+__device__ __forceinline__ uint32_t group_bits8(uint64_t m) {
+  m &= 0x8040201008040201ull;
+  m |= m >> 32;
+  m |= m >> 16;
+  m |= m >> 8;
+  return (uint32_t)(m & 0xFFu);
+}
+// OR the bits of a 32-bit tile mask (bit i = vertex v0 + i) into bitmap bm (one lane)
+__device__ __forceinline__ void tile_mask_or(uint32_t* bm, int32_t v0, uint32_t m) {
+  if (!m) return;
+  const int32_t w = v0 >> 5, sh = v0 & 31;
+  atomicOr(&bm[w], m << sh);
+  if (sh && (m >> (32 - sh))) atomicOr(&bm[w + 1], m >> (32 - sh));
+}
+
+// zrow: an all-zero row (the gather target of the idle lane groups of a batch)
 template <int W>
 __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
     const PfxTile* __restrict__ tiles, int64_t ntiles, const uint32_t* __restrict__ pent,
     int nparts, const int64_t* rowptr, const uint64_t* R, uint64_t* O, uint64_t* acc,
     const uint32_t* pvis, const uint32_t* snap, const uint32_t* code, int32_t code_from,
     const uint64_t* alive, const uint64_t* gmask, uint32_t* done, uint32_t* anyvis, uint32_t* fbm,
-    const int32_t* stamp, int32_t epoch, Ctr* ctr, uint32_t* slabF) {
+    const int32_t* stamp, int32_t epoch, Ctr* ctr, uint32_t* slabF, const uint64_t* zrow,
+    int exp) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, S = 64 / G, VT = kTileVT;
+  static_assert(G == 8 && VPW == 8, "the tile masks take 8 vertices per epilogue pass");
   constexpr int NWV = kTileBlock / 64;
-  constexpr int PB = 4;       // rows in flight per lane group
-  constexpr int Q = 4;        // entries per lane per round
+  constexpr int PB = 4;       // rows in flight per lane group and batch
+  constexpr int Q = kRoundQ;
   constexpr int CR = 65;      // bank-skewed counter rows (BitCounter::spill_strided)
+  constexpr int YW = VT * W + 64;  // + one dummy word per lane (idle lanes' ORs, no conflicts)
   __shared__ uint32_t hub[kTileHubW];
-  __shared__ unsigned long long Y[NWV][VT * W];
-  __shared__ uint32_t lst[NWV][64 * Q];
+  __shared__ unsigned long long Y[NWV][YW];
+  __shared__ uint32_t lst[NWV][kRound];
   __shared__ uint32_t cnt[CR * W];
   __shared__ unsigned long long scratch[NWV];
   __shared__ uint32_t scratch32[NWV];
@@ -113,158 +154,213 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
   __syncthreads();
   const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
   unsigned long long* y = Y[wv];
+  const int dummy = VT * W + lane;
   uint32_t* ls = lst[wv];
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  unsigned long long ef = 0, ev = 0;
+  unsigned long long ef = 0, ev = 0, sink = 0;
   uint32_t nfc = 0;
-  BitCounter<VW> bc;
+  BitCounter<VW, 4> bc;  // (4 slices: spills every 15 passes, 8 fewer VGPRs than 6)
   bc.zero();
   int nadd = 0;
-  const int64_t wave = (int64_t)blockIdx.x * NWV + wv;
   const int64_t nwaves = (int64_t)gridDim.x * NWV;
-  for (int64_t t = wave; t < ntiles; t += nwaves) {
-    const int32_t v0 = uni32(tiles[t].v0);
-    const int32_t nvf = uni32(tiles[t].nv);
-    const int64_t e0 = uni64(tiles[t].e0), e1 = uni64(tiles[t + 1].e0);
-    const int nv = (nvf & kTilePartial) ? 1 : (nvf & 0xFFFF);
+  auto load_round = [&](const TileRound& r, uint32_t (&pk)[Q]) {
 #pragma unroll
-    for (int k = lane; k < VT * W; k += 64) y[k] = 0;
-    __builtin_amdgcn_wave_barrier();
-    for (int64_t e = e0; e < e1; e += 64 * Q) {
-      uint32_t pk[Q];
+    for (int q = 0; q < Q; ++q) {
+      const int64_t i = r.e + q * 64 + lane;
+      pk[q] = (r.t < ntiles && i < r.e1) ? pent[i] : kPentNone;
+    }
+  };
+  // probe (branch-free: the unused lanes read hub word 0) + code loads of a round
+  auto probe_round = [&](uint32_t (&pk)[Q], uint32_t (&cd)[Q]) {
 #pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int64_t i = e + q * 64 + lane;
-        pk[q] = i < e1 ? pent[i] : kPentNone;
-      }
-      // visited hubs only (the LDS bitmap: any-visited at the level start)
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t u = pk[q] != kPentNone ? pk[q] & kPentUMask : 0u;
+      const bool hit = (hub[u >> 5] >> (u & 31)) & 1u;
+      pk[q] = hit ? pk[q] : kPentNone;
+    }
 #pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (pk[q] != kPentNone) {
-          const uint32_t u = pk[q] & kPentUMask;
-          if (!((hub[u >> 5] >> (u & 31)) & 1u)) pk[q] = kPentNone;
-        }
-      // sparse codes: the bits go straight into the accumulator rows
-      uint32_t cd[Q];
+    for (int q = 0; q < Q; ++q) cd[q] = kDenseCode;
+    if (code_from != INT32_MAX) {  // (uniform: no codes on this level, no code array)
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        cd[q] = kDenseCode;
-        if (pk[q] != kPentNone && (int32_t)(pk[q] & kPentUMask) >= code_from)
-          cd[q] = code[pk[q] & kPentUMask];
+        const uint32_t u = pk[q] & kPentUMask;
+        const bool coded = pk[q] != kPentNone && (int32_t)u >= code_from;
+        const uint32_t c = code[coded ? u : (uint32_t)code_from];
+        cd[q] = coded ? c : kDenseCode;
       }
+    }
+  };
+  TileRound rc = tile_first_round(tiles, ntiles, (int64_t)blockIdx.x * NWV + wv);
+  TileRound rb = tile_next_round(tiles, ntiles, nwaves, rc);
+  uint32_t pkc[Q], cdc[Q], pkb[Q], cdb[Q], pka[Q];
+  load_round(rc, pkc);
+  load_round(rb, pkb);
+  probe_round(pkc, cdc);
+  while (rc.t < ntiles) {
+    const TileRound ra = tile_next_round(tiles, ntiles, nwaves, rb);
+    probe_round(pkb, cdb);  // codes of round r + 1 in flight
+    load_round(ra, pka);    // entries of round r + 2 in flight
+    if (rc.e == rc.e0) {    // first round of a tile: clear the accumulator rows
 #pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (pk[q] != kPentNone && cd[q] != kDenseCode) {
-          const int vl = (int)(pk[q] >> kPentUBits);
-#pragma unroll
-          for (int i = 0; i < kCodeSlots; ++i) {
-            const int g = code_g(cd[q], i);
-            if (g >= 0) atomicOr(&y[vl * W + (g >> 6)], 1ull << (g & 63));
-          }
-          pk[q] = kPentNone;
-        }
-      // the rest: dense rows, compacted into the wave's list
-      int c = 0;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const bool keep = pk[q] != kPentNone;
-        const uint64_t m = __ballot(keep);
-        if (keep) ls[c + __popcll(m & lanemask_lt())] = pk[q];
-        c += __popcll(m);
-      }
-      __builtin_amdgcn_wave_barrier();
-      for (int b = 0; b < c; b += PB * S) {
-        uint32_t uu[PB];
-#pragma unroll
-        for (int q = 0; q < PB; ++q) {
-          const int k = b + q * S + sub;
-          uu[q] = k < c ? ls[k] : kPentNone;
-        }
-        V<VW> x[PB];
-#pragma unroll
-        for (int q = 0; q < PB; ++q)
-          x[q] = uu[q] != kPentNone
-                     ? ldv<VW>(R + (int64_t)(uu[q] & kPentUMask) * W + slot * VW)
-                     : vzero<VW>();
-#pragma unroll
-        for (int q = 0; q < PB; ++q)
-          if (uu[q] != kPentNone) {
-            const int vl = (int)(uu[q] >> kPentUBits);
-#pragma unroll
-            for (int j = 0; j < VW; ++j)
-              if (x[q].w[j]) atomicOr(&y[vl * W + slot * VW + j], x[q].w[j]);
-          }
-      }
+      for (int k = lane; k < VT * W; k += 64) y[k] = 0;
       __builtin_amdgcn_wave_barrier();
     }
-    if (nvf & kTilePartial) {
-      // a slice of a big vertex: publish its bits (k_bu_wide_finalize folds them in)
-      if (sub == 0) {
-        const int64_t vo = (int64_t)v0 * W + slot * VW;
+    // ---- round r: sparse codes straight into the accumulator rows (idle slots: dummy word)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const bool coded = pkc[q] != kPentNone && cdc[q] != kDenseCode;
+      const int vl = (int)(pkc[q] >> kPentUBits);
+#pragma unroll
+      for (int i = 0; i < kCodeSlots; ++i) {
+        const int g = coded ? code_g(cdc[q], i) : -1;
+        if (!(exp & 2))  // (timing experiment: no code ORs)
+          atomicOr(&y[g >= 0 ? vl * W + (g >> 6) : dummy], g >= 0 ? 1ull << (g & 63) : 0ull);
+      }
+      pkc[q] = coded ? kPentNone : pkc[q];
+    }
+    // the rest: dense rows, compacted into the wave's list, gathered by lane groups
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const bool keep = pkc[q] != kPentNone;
+      const uint64_t m = __ballot(keep);
+      if (keep) ls[c + __popcll(m & lanemask_lt())] = pkc[q];
+      c += __popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int b = 0; b < ((exp & 4) ? 0 : c); b += PB * S) {  // (exp 4: no row gathers)
+      uint32_t uu[PB];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int k = b + q * S + sub;
+        uu[q] = ls[k < c ? k : 0];
+        uu[q] = k < c ? uu[q] : kPentNone;
+      }
+      V<VW> x[PB];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const uint64_t* src = uu[q] != kPentNone
+                                  ? R + (int64_t)(uu[q] & kPentUMask) * W + slot * VW
+                                  : zrow + slot * VW;
+        x[q] = ldv<VW>(src);
+      }
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int base = uu[q] != kPentNone ? (int)(uu[q] >> kPentUBits) * W + slot * VW : -1;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
-          const uint64_t a = y[slot * VW + j];
-          if (a) atomicOr((unsigned long long*)&acc[vo + j], a);
+          if (!(exp & 1)) atomicOr(&y[base >= 0 ? base + j : dummy], x[q].w[j]);
+          else sink ^= x[q].w[j];  // (timing experiment: no row ORs)
         }
       }
-      continue;
     }
-    // epilogue: VPW vertices per pass, G lanes each (the narrow pull's, without list queues)
-    for (int p = 0; p < nv; p += VPW) {
-      const int i = p + sub;
-      const int32_t v = v0 + i * nparts;
-      bool valid = i < nv;
-      uint32_t deg = 0;
-      if (valid) {
-        deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
-        valid = deg > 0 && !is_done(done, v);
-      }
-      V<VW> r = vzero<VW>(), a = vzero<VW>();
-      if (valid) {
-        const int64_t vo = (int64_t)v * W + slot * VW;
-        if (!(snap && !any_visited(snap, v))) r = ldv<VW>(R + vo);
+    __builtin_amdgcn_wave_barrier();
+    if (rc.e + kRound >= rc.e1) {  // last round of the tile
+      const int32_t v0 = uni32(tiles[rc.t].v0);
+      const int32_t nvf = uni32(tiles[rc.t].nv);
+      if (nvf & kTilePartial) {
+        // a slice of a big vertex: publish its bits (k_bu_wide_finalize folds them in)
+        if (sub == 0) {
+          const int64_t vo = (int64_t)v0 * W + slot * VW;
 #pragma unroll
-        for (int j = 0; j < VW; ++j) a.w[j] = y[i * W + slot * VW + j];
-        if (stamp[v] == epoch) {  // bits pushed from the tail frontier (k_push_tail)
-          const V<VW> pa = ldv<VW>(acc + vo);
+          for (int j = 0; j < VW; ++j) {
+            const uint64_t a = y[slot * VW + j];
+            if (a) atomicOr((unsigned long long*)&acc[vo + j], a);
+          }
+        }
+      } else {
+        // epilogue: VPW vertices per pass, G lanes each (the narrow pull's, without list
+        // queues); done / frontier / first-visit bits collect in tile masks (bit i = vertex i)
+        const int nv = nvf & 0xFFFF;
+        uint32_t m_done = 0, m_new = 0, m_first = 0;
+        for (int p = 0; p < nv; p += VPW) {
+          const int i = p + sub;
+          const int32_t v = v0 + i * nparts;
+          bool valid = i < nv;
+          uint32_t deg = 0;
+          if (valid) {
+            deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
+            valid = deg > 0 && !is_done(done, v);
+          }
+          V<VW> r = vzero<VW>(), a = vzero<VW>();
+          if (valid) {
+            const int64_t vo = (int64_t)v * W + slot * VW;
+            if (!(snap && !any_visited(snap, v))) r = ldv<VW>(R + vo);
 #pragma unroll
-          for (int j = 0; j < VW; ++j) a.w[j] |= pa.w[j];
-          stv<VW>(acc + vo, vzero<VW>());
+            for (int j = 0; j < VW; ++j) a.w[j] = y[i * W + slot * VW + j];
+            if (stamp[v] == epoch) {  // bits pushed from the tail frontier (k_push_tail)
+              const V<VW> pa = ldv<VW>(acc + vo);
+#pragma unroll
+              for (int j = 0; j < VW; ++j) a.w[j] |= pa.w[j];
+              stv<VW>(acc + vo, vzero<VW>());
+            }
+          }
+          V<VW> nw, nvr;
+          bool anynew = false, notfull = false, rnz = false;
+#pragma unroll
+          for (int j = 0; j < VW; ++j) {
+            const uint64_t unv = ~r.w[j] & am.w[j];
+            nw.w[j] = valid ? a.w[j] & unv : 0;
+            nvr.w[j] = r.w[j] | nw.w[j];
+            anynew |= nw.w[j] != 0;
+            notfull |= (unv & ~nw.w[j]) != 0;
+            rnz |= r.w[j] != 0;
+          }
+          if (valid) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
+          bc.add(nw);
+          if (++nadd == (1 << 4) - 1) {
+            bc.template spill_strided<CR>(cnt, slot);
+            nadd = 0;
+          }
+          const uint64_t bval = __ballot(valid), bnew = __ballot(anynew);
+          const uint64_t bnf = __ballot(notfull), brnz = __ballot(rnz);
+          // (group-uniform bytes: a group's lanes share validity; OR-ed words -> whole byte)
+          auto grp = [](uint64_t m) {
+            m |= (m >> 1) & 0x7F7F7F7F7F7F7F7Full;
+            m |= (m >> 2) & 0x3F3F3F3F3F3F3F3Full;
+            m |= (m >> 4) & 0x0F0F0F0F0F0F0F0Full;  // bit 8k = OR of byte k
+            return (m & 0x0101010101010101ull) * 0xFFull;
+          };
+          const uint64_t gval = grp(bval), gnew = grp(bnew) & gval;
+          const uint64_t gnf = grp(bnf), gfirst = gnew & ~grp(brnz);
+          m_done |= group_bits8(gval & ~gnf) << p;
+          m_new |= group_bits8(gnew) << p;
+          m_first |= group_bits8(gfirst) << p;
+          const bool g_new = (gnew >> (sub * G)) & 1ull, g_first = (gfirst >> (sub * G)) & 1ull;
+          const bool leader = valid && slot == 0;
+          if (leader && g_new) {
+            ++nfc;
+            ef += deg;
+          }
+          if (leader && g_first) ev += deg;
+        }
+        if (nparts == 1) {
+          if (lane == 0) {
+            tile_mask_or(done, v0, m_done);
+            tile_mask_or(fbm, v0, m_new);
+            tile_mask_or(anyvis, v0, m_first);
+          }
+        } else if (lane < nv) {  // (hybrid phase A: strided vertices, one bit each)
+          const int32_t v = v0 + lane * nparts;
+          if ((m_done >> lane) & 1u) atomicOr(&done[v >> 5], 1u << (v & 31));
+          if ((m_new >> lane) & 1u) atomicOr(&fbm[v >> 5], 1u << (v & 31));
+          if ((m_first >> lane) & 1u) atomicOr(&anyvis[v >> 5], 1u << (v & 31));
         }
       }
-      V<VW> nw, nvr;
-      bool anynew = false, notfull = false, rnz = false;
+    }
+    // shift the pipeline
+    rc = rb;
+    rb = ra;
 #pragma unroll
-      for (int j = 0; j < VW; ++j) {
-        const uint64_t unv = ~r.w[j] & am.w[j];
-        nw.w[j] = valid ? a.w[j] & unv : 0;
-        nvr.w[j] = r.w[j] | nw.w[j];
-        anynew |= nw.w[j] != 0;
-        notfull |= (unv & ~nw.w[j]) != 0;
-        rnz |= r.w[j] != 0;
-      }
-      if (valid) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
-      bc.add(nw);
-      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
-        bc.template spill_strided<CR>(cnt, slot);
-        nadd = 0;
-      }
-      const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
-      const bool g_nf = (__ballot(notfull) >> (sub * G)) & L::GBITS;
-      const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
-      const bool leader = valid && slot == 0;
-      wave_set_bits<true>(done, v, leader && !g_nf);
-      wave_set_bits<true>(fbm, v, leader && g_new);
-      wave_set_bits<true>(anyvis, v, leader && g_first);
-      if (leader && g_new) {
-        ++nfc;
-        ef += deg;
-      }
-      if (leader && g_first) ev += deg;
+    for (int q = 0; q < Q; ++q) {
+      pkc[q] = pkb[q];
+      cdc[q] = cdb[q];
+      pkb[q] = pka[q];
     }
   }
+  if (sink == 0x5a5a5a5a5a5a5a5aull) ctr->touched.v = 1;  // (keeps exp 1's loads)
   block_sum_add32(nfc, &ctr->fl2.v, scratch32);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);

@@ -61,11 +61,16 @@ __global__ void k_gather_plen(const int32_t* plen, int64_t cnt, int part, int np
 
 const BitparSolver::TileSet* BitparSolver::pfx_tiles(int W, int part, int nparts, hipStream_t s) {
   if (!tiles_ok_ || !tun_.tiles) return nullptr;
-  TileSet& T = tiles_;
-  if (W < 8) return nullptr;
-  if (T.key[0] == (const void*)g_.rowptr && T.key[1] == (const void*)g_.col &&
-      T.part == part && T.nparts == nparts)
-    return &T;
+  if (W != 16) return nullptr;  // (k_pfx_tiles: 8 lanes per vertex)
+  for (auto it = tilesets_.begin(); it != tilesets_.end();) {
+    TileSet& T = **it;
+    if (T.key[0] != (const void*)g_.rowptr || T.key[1] != (const void*)g_.col) {
+      it = tilesets_.erase(it);  // (an older graph buffer: relabelled or replaced)
+      continue;
+    }
+    if (T.part == part && T.nparts == nparts) return &T;
+    ++it;
+  }
   constexpr int32_t kPfxH = kTileHubW * 32;
   const int32_t* plen = prefix_lens(kPfxH, s);
   const int64_t ne = n_eff(), cnt = ne > part ? (ne - part + nparts - 1) / nparts : 0;
@@ -85,18 +90,20 @@ const BitparSolver::TileSet* BitparSolver::pfx_tiles(int W, int part, int nparts
   std::vector<int32_t> big;
   int64_t nent = 0;
   greedy_tiles(hp, cnt, part, nparts, tl, big, nent);
-  T.pent.release();
-  T.tiles.release();
-  T.big.release();
-  T.key[0] = T.key[1] = nullptr;
   const size_t pb = (size_t)std::max<int64_t>(nent, 1) * sizeof(uint32_t);
   const size_t tb = tl.size() * sizeof(PfxTile), bb = std::max<size_t>(big.size(), 1) * 4;
   size_t fr = 0, tot = 0;
   MSBFS_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+  if (pb + tb + bb + ((size_t)4 << 30) > fr && !tilesets_.empty()) {
+    tilesets_.clear();  // (another partition's tiles: make room)
+    MSBFS_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+  }
   if (pb + tb + bb + ((size_t)4 << 30) > fr) {  // (RMAT-30: keep the per-vertex pulls)
     tiles_ok_ = false;
     return nullptr;
   }
+  tilesets_.push_back(std::make_unique<TileSet>());
+  TileSet& T = *tilesets_.back();
   T.pent.alloc(pb);
   T.tiles.alloc(tb);
   T.big.alloc(bb);
@@ -122,6 +129,10 @@ const BitparSolver::TileSet* BitparSolver::pfx_tiles(int W, int part, int nparts
     num_cus_ = prop.multiProcessorCount;
   }
   fbm_tile_.ensure((size_t)((g_.n + 31) / 32 + 1) * sizeof(uint32_t));
+  if (!zrow_.p) {
+    zrow_.alloc(16 * sizeof(uint64_t));
+    MSBFS_HIP_CHECK(hipMemsetAsync(zrow_.p, 0, zrow_.bytes, s));
+  }
   lcnt_.ensure(sizeof(Ctr));
   return &T;
 }
@@ -133,8 +144,8 @@ template <int W>
 int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t* O,
                              const uint32_t* snap, const uint32_t* codes, int32_t code_from,
                              int rows) {
-  if constexpr (W < 8) {
-    fail("tiled pull: needs 8 or 16 words");
+  if constexpr (W != 16) {
+    fail("tiled pull: needs 16 words");
   } else {
   const TileSet* T = pfx_tiles(W, S.part, S.nparts, s);
   const Small sm = small();
@@ -147,7 +158,8 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
       T->tiles.as<PfxTile>(), T->ntiles, T->pent.as<uint32_t>(), S.nparts, g_.rowptr, R, O,
       acc_[S.ac].as<uint64_t>(), pvis, snap, codes, codes ? code_from : INT32_MAX, alive,
       sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), fbm_tile_.as<uint32_t>(),
-      stamp_.as<int32_t>(), epoch_, ctr_.as<Ctr>(), slabF<W>(rows));
+      stamp_.as<int32_t>(), epoch_, ctr_.as<Ctr>(), slabF<W>(rows), zrow_.as<uint64_t>(),
+      tun_.tiles_exp);
   MSBFS_HIP_CHECK(hipGetLastError());
   rows += grid;
   if (T->nbig) {
