@@ -89,9 +89,8 @@ __global__ __launch_bounds__(256) void k_fill_pent(const PfxTile* tiles, int64_t
 }
 
 // One round = up to kRound entries of one tile. Rounds are software-pipelined across the
-// wave's tiles (tile t, t + nwaves, ...): while round r is processed, the codes of round r + 1
-// and the packed entries of round r + 2 are in flight, so a round waits for its row gathers
-// only (the entry stream comes from HBM, the codes from L2).
+// wave's tiles (tile t, t + nwaves, ...): while round r is processed, the packed entries of
+// round r + 1 are in flight (the entry stream comes from HBM).
 constexpr int kRoundQ = 4;                 // entries per lane per round
 constexpr int kRound = 64 * kRoundQ;
 struct TileRound {
@@ -161,7 +160,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long ef = 0, ev = 0, sink = 0;
   uint32_t nfc = 0;
-  BitCounter<VW, 4> bc;  // (4 slices: spills every 15 passes, 8 fewer VGPRs than 6)
+  BitCounter<VW, 3> bc;  // (3 slices: spills every 7 passes, 12 fewer VGPRs than 6)
   bc.zero();
   int nadd = 0;
   const int64_t nwaves = (int64_t)gridDim.x * NWV;
@@ -193,15 +192,12 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
     }
   };
   TileRound rc = tile_first_round(tiles, ntiles, (int64_t)blockIdx.x * NWV + wv);
-  TileRound rb = tile_next_round(tiles, ntiles, nwaves, rc);
-  uint32_t pkc[Q], cdc[Q], pkb[Q], cdb[Q], pka[Q];
+  TileRound rb = tile_next_round(tiles, ntiles, nwaves, rc);  // (rc's successor)
+  uint32_t pkc[Q], cdc[Q], pkb[Q];
   load_round(rc, pkc);
-  load_round(rb, pkb);
-  probe_round(pkc, cdc);
   while (rc.t < ntiles) {
-    const TileRound ra = tile_next_round(tiles, ntiles, nwaves, rb);
-    probe_round(pkb, cdb);  // codes of round r + 1 in flight
-    load_round(ra, pka);    // entries of round r + 2 in flight
+    load_round(rb, pkb);    // entries of round r + 1 in flight
+    probe_round(pkc, cdc);
     if (rc.e == rc.e0) {    // first round of a tile: clear the accumulator rows
 #pragma unroll
       for (int k = lane; k < VT * W; k += 64) y[k] = 0;
@@ -257,7 +253,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
       }
     }
     __builtin_amdgcn_wave_barrier();
-    if (rc.e + kRound >= rc.e1) {  // last round of the tile
+    if (rc.e + kRound >= rc.e1 && !(exp & 8)) {  // last round of the tile (exp 8: no epilogue)
       const int32_t v0 = uni32(tiles[rc.t].v0);
       const int32_t nvf = uni32(tiles[rc.t].nv);
       if (nvf & kTilePartial) {
@@ -272,30 +268,63 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
         }
       } else {
         // epilogue: VPW vertices per pass, G lanes each (the narrow pull's, without list
-        // queues); done / frontier / first-visit bits collect in tile masks (bit i = vertex i)
+        // queues); done / frontier / first-visit bits collect in tile masks (bit i = vertex i).
+        // Every load of the tile is issued before any is used: lane i fetches vertex i's row
+        // offsets, stamp and bitmap words, every lane group its vertices' own rows; then the
+        // pushed rows of the stamped vertices (one dependent round trip per tile, not per pass).
         const int nv = nvf & 0xFFFF;
+        constexpr int NP = kTileVT / VPW;  // passes per tile
+        const int32_t vlane = v0 + lane * nparts;
+        int64_t rp0 = 0, rp1 = 0;
+        int32_t stl = 0;
+        uint32_t dwl = 0, swl = ~0u;
+        if (lane < nv) {
+          rp0 = rowptr[vlane];
+          rp1 = rowptr[vlane + 1];
+          stl = stamp[vlane];
+          dwl = done[vlane >> 5];
+          swl = (snap ? snap : anyvis)[vlane >> 5];
+        }
+        const uint32_t degl = (uint32_t)(rp1 - rp0);
+        const bool okl = lane < nv && degl > 0 && !((dwl >> (vlane & 31)) & 1u);
+        // own row: only a vertex some group visited has a non-zero row (and in a lazy batch the
+        // row of one nobody visited is stale): at level 2 that skips ~99 % of the own-row loads.
+        // (anyvis bits of this tile's vertices change only in this epilogue, after the read)
+        const bool visl = lane < nv && ((swl >> (vlane & 31)) & 1u);
+        const bool pushl = okl && stl == epoch;         // bits pushed by k_push_tail
+        const uint64_t bok = __ballot(okl), bvis = __ballot(visl), bpush = __ballot(pushl);
         uint32_t m_done = 0, m_new = 0, m_first = 0;
-        for (int p = 0; p < nv; p += VPW) {
-          const int i = p + sub;
-          const int32_t v = v0 + i * nparts;
-          bool valid = i < nv;
-          uint32_t deg = 0;
-          if (valid) {
-            deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
-            valid = deg > 0 && !is_done(done, v);
-          }
-          V<VW> r = vzero<VW>(), a = vzero<VW>();
-          if (valid) {
-            const int64_t vo = (int64_t)v * W + slot * VW;
-            if (!(snap && !any_visited(snap, v))) r = ldv<VW>(R + vo);
+        // two passes per batch: own rows and pushed rows of 16 vertices in flight
+        constexpr int NH = 1;
 #pragma unroll
-            for (int j = 0; j < VW; ++j) a.w[j] = y[i * W + slot * VW + j];
-            if (stamp[v] == epoch) {  // bits pushed from the tail frontier (k_push_tail)
-              const V<VW> pa = ldv<VW>(acc + vo);
+        for (int h = 0; h < NP; h += NH) {
+          if (h * VPW >= nv) break;
+          V<VW> rr[NH], pa[NH];
 #pragma unroll
-              for (int j = 0; j < VW; ++j) a.w[j] |= pa.w[j];
+          for (int k = 0; k < NH; ++k) {
+            const int i = (h + k) * VPW + sub;
+            const int64_t vo = (int64_t)(v0 + i * nparts) * W + slot * VW;
+            rr[k] = ((bvis >> i) & 1ull) ? ldv<VW>(R + vo) : vzero<VW>();
+            pa[k] = vzero<VW>();
+            if ((bpush >> i) & 1ull) {
+              pa[k] = ldv<VW>(acc + vo);
               stv<VW>(acc + vo, vzero<VW>());
             }
+          }
+#pragma unroll
+        for (int k = 0; k < NH; ++k) {
+          const int pi = h + k;
+          const int p = pi * VPW;
+          if (p >= nv) break;
+          const int i = p + sub;
+          const int32_t v = v0 + i * nparts;
+          const bool valid = (bok >> i) & 1ull;
+          const uint32_t deg = (uint32_t)__shfl((int)degl, i);
+          V<VW> r = vzero<VW>(), a = vzero<VW>();
+          if (valid) {
+            r = rr[k];
+#pragma unroll
+            for (int j = 0; j < VW; ++j) a.w[j] = y[i * W + slot * VW + j] | pa[k].w[j];
           }
           V<VW> nw, nvr;
           bool anynew = false, notfull = false, rnz = false;
@@ -309,8 +338,8 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
             rnz |= r.w[j] != 0;
           }
           if (valid) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
-          bc.add(nw);
-          if (++nadd == (1 << 4) - 1) {
+          if (!(exp & 16)) bc.add(nw);  // (exp 16: no counting)
+          if (++nadd == (1 << 3) - 1) {
             bc.template spill_strided<CR>(cnt, slot);
             nadd = 0;
           }
@@ -336,6 +365,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           }
           if (leader && g_first) ev += deg;
         }
+        }
         if (nparts == 1) {
           if (lane == 0) {
             tile_mask_or(done, v0, m_done);
@@ -352,13 +382,9 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
     }
     // shift the pipeline
     rc = rb;
-    rb = ra;
+    rb = tile_next_round(tiles, ntiles, nwaves, rb);
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      pkc[q] = pkb[q];
-      cdc[q] = cdb[q];
-      pkb[q] = pka[q];
-    }
+    for (int q = 0; q < Q; ++q) pkc[q] = pkb[q];
   }
   if (sink == 0x5a5a5a5a5a5a5a5aull) ctr->touched.v = 1;  // (keeps exp 1's loads)
   block_sum_add32(nfc, &ctr->fl2.v, scratch32);

@@ -186,7 +186,8 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   if (first_bu && S.level == 2 && tun_.codes && W >= 8 && S.ef0 > 0 && n <= INT32_MAX) {
     const int64_t ne = n_eff();
     code_from = (int32_t)std::min<int64_t>(
-        code_bound(tun_.code_deg * (double)g_.nnz / (double)S.ef0), ne);
+        code_bound((tiled ? tun_.tiles_code_deg : tun_.code_deg) * (double)g_.nnz /
+                   (double)S.ef0), ne);
     if (code_from < ne) {
       uint32_t* cb = touched_.as<uint32_t>();  // n entries
       const int64_t hi = pfx ? std::min<int64_t>(std::max<int64_t>(kPfxH, code_from), ne) : ne;
