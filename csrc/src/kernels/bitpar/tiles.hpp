@@ -155,12 +155,15 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
   unsigned long long* y = Y[wv];
   const int dummy = VT * W + lane;
   uint32_t* ls = lst[wv];
-  V<VW> am;
-#pragma unroll
-  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  unsigned long long ef = 0, ev = 0, sink = 0;
+  // alive & batch mask per word in LDS (read per epilogue pass: registers go to the counters)
+  __shared__ unsigned long long amask[W];
+  if (threadIdx.x < W) amask[threadIdx.x] = alive[threadIdx.x] & gmask[threadIdx.x];
+  __syncthreads();
+  unsigned long long ef = 0, ev = 0;
   uint32_t nfc = 0;
-  BitCounter<VW, 3> bc;  // (3 slices: spills every 7 passes, 12 fewer VGPRs than 6)
+  // 4 slices: a spill (one LDS add per set counter bit, ~100 per lane at level 2) every 15
+  // passes (3 slices: every 7; 5 do not fit the 128 VGPRs of a 1024-thread block)
+  BitCounter<VW, 4> bc;
   bc.zero();
   int nadd = 0;
   const int64_t nwaves = (int64_t)gridDim.x * NWV;
@@ -246,10 +249,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
       for (int q = 0; q < PB; ++q) {
         const int base = uu[q] != kPentNone ? (int)(uu[q] >> kPentUBits) * W + slot * VW : -1;
 #pragma unroll
-        for (int j = 0; j < VW; ++j) {
-          if (!(exp & 1)) atomicOr(&y[base >= 0 ? base + j : dummy], x[q].w[j]);
-          else sink ^= x[q].w[j];  // (timing experiment: no row ORs)
-        }
+        for (int j = 0; j < VW; ++j) atomicOr(&y[base >= 0 ? base + j : dummy], x[q].w[j]);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           bool anynew = false, notfull = false, rnz = false;
 #pragma unroll
           for (int j = 0; j < VW; ++j) {
-            const uint64_t unv = ~r.w[j] & am.w[j];
+            const uint64_t unv = ~r.w[j] & amask[slot * VW + j];
             nw.w[j] = valid ? a.w[j] & unv : 0;
             nvr.w[j] = r.w[j] | nw.w[j];
             anynew |= nw.w[j] != 0;
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           }
           if (valid) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
           if (!(exp & 16)) bc.add(nw);  // (exp 16: no counting)
-          if (++nadd == (1 << 3) - 1) {
+          if (++nadd == (1 << 4) - 1) {
             bc.template spill_strided<CR>(cnt, slot);
             nadd = 0;
           }
@@ -386,7 +386,6 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
 #pragma unroll
     for (int q = 0; q < Q; ++q) pkc[q] = pkb[q];
   }
-  if (sink == 0x5a5a5a5a5a5a5a5aull) ctr->touched.v = 1;  // (keeps exp 1's loads)
   block_sum_add32(nfc, &ctr->fl2.v, scratch32);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);

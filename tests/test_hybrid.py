@@ -258,6 +258,24 @@ def test_hybrid_matches_cpu_other_graphs(msbfs_pkg, world):
 
 
 @pytest.mark.gpu
+def test_hybrid_tiled_phase_a(msbfs_pkg):
+    """Phase A's level 2 over the static tiles of each rank's strided vertex set (RMAT-23: large
+    enough for the prefix pull; one tile set per emulated rank): F equal to the standard solver
+    with the tiles on and off, for several rank counts in a row (cached tile sets reused)."""
+    m = msbfs_pkg
+    H = _H()
+    dg = m.DeviceGraph.rmat(23, 16, 5, device=0, relabel=True)
+    qs = m.QuerySet.random(dg.n, 1024, 16, seed=23)
+    with m.Solver(dg, "bitpar", max_groups=1024, tuning={"tiles": 0}) as s:
+        ref = s.run(qs).F
+    with m.Solver(dg, "bitpar", max_groups=1024) as s:
+        assert np.array_equal(s.run(qs).F, ref)
+        for world in (2, 3, 8, 2):
+            assert np.array_equal(H.emulate_ranks(s, qs, world), ref), world
+    dg.close()
+
+
+@pytest.mark.gpu
 def test_hybrid_lazy_reset_with_stale_rows(msbfs_pkg):
     """Phase A skips the visited-buffer fill (k_zero_part_rows + the top-down anyvis guard): run
     it over buffers full of another query set's rows (a normal run, then other phases) and check
