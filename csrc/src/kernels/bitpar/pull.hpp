@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void k_push_tail(
           if (w) atomicOr((unsigned long long*)&acc[(int64_t)v * W + j], (unsigned long long)w);
         }
       }
-      stamp[v] = epoch;
+      if (stamp) stamp[v] = epoch;  // (nullptr: the tiled pull reads every acc row instead)
     }
   }
 }

@@ -132,8 +132,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
     int nparts, const int64_t* rowptr, const uint64_t* R, uint64_t* O, uint64_t* acc,
     const uint32_t* pvis, const uint32_t* snap, const uint32_t* code, int32_t code_from,
     const uint64_t* alive, const uint64_t* gmask, uint32_t* done, uint32_t* anyvis, uint32_t* fbm,
-    const int32_t* stamp, int32_t epoch, Ctr* ctr, uint32_t* slabF, const uint64_t* zrow,
-    int exp) {
+    Ctr* ctr, uint32_t* slabF, const uint64_t* zrow, int exp) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, S = 64 / G, VT = kTileVT;
   static_assert(G == 8 && VPW == 8, "the tile masks take 8 vertices per epilogue pass");
@@ -276,12 +275,10 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
         constexpr int NP = kTileVT / VPW;  // passes per tile
         const int32_t vlane = v0 + lane * nparts;
         int64_t rp0 = 0, rp1 = 0;
-        int32_t stl = 0;
         uint32_t dwl = 0, swl = ~0u;
         if (lane < nv) {
           rp0 = rowptr[vlane];
           rp1 = rowptr[vlane + 1];
-          stl = stamp[vlane];
           dwl = done[vlane >> 5];
           swl = (snap ? snap : anyvis)[vlane >> 5];
         }
@@ -291,8 +288,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
         // row of one nobody visited is stale): at level 2 that skips ~99 % of the own-row loads.
         // (anyvis bits of this tile's vertices change only in this epilogue, after the read)
         const bool visl = lane < nv && ((swl >> (vlane & 31)) & 1u);
-        const bool pushl = okl && stl == epoch;         // bits pushed by k_push_tail
-        const uint64_t bok = __ballot(okl), bvis = __ballot(visl), bpush = __ballot(pushl);
+        const uint64_t bok = __ballot(okl), bvis = __ballot(visl);
         uint32_t m_done = 0, m_new = 0, m_first = 0;
         // two passes per batch: own rows and pushed rows of 16 vertices in flight
         constexpr int NH = 1;
@@ -305,11 +301,9 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
             const int i = (h + k) * VPW + sub;
             const int64_t vo = (int64_t)(v0 + i * nparts) * W + slot * VW;
             rr[k] = ((bvis >> i) & 1ull) ? ldv<VW>(R + vo) : vzero<VW>();
-            pa[k] = vzero<VW>();
-            if ((bpush >> i) & 1ull) {
-              pa[k] = ldv<VW>(acc + vo);
-              stv<VW>(acc + vo, vzero<VW>());
-            }
+            // bits pushed by k_push_tail (no stamps: the level's acc rows are all-zero but
+            // the pushed ones, and a tile's rows are one contiguous run)
+            pa[k] = ((bok >> i) & 1ull) ? ldv<VW>(acc + vo) : vzero<VW>();
           }
 #pragma unroll
         for (int k = 0; k < NH; ++k) {
@@ -323,8 +317,13 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           V<VW> r = vzero<VW>(), a = vzero<VW>();
           if (valid) {
             r = rr[k];
+            bool pushed = false;
 #pragma unroll
-            for (int j = 0; j < VW; ++j) a.w[j] = y[i * W + slot * VW + j] | pa[k].w[j];
+            for (int j = 0; j < VW; ++j) {
+              a.w[j] = y[i * W + slot * VW + j] | pa[k].w[j];
+              pushed |= pa[k].w[j] != 0;
+            }
+            if (pushed) stv<VW>(acc + (int64_t)v * W + slot * VW, vzero<VW>());
           }
           V<VW> nw, nvr;
           bool anynew = false, notfull = false, rnz = false;

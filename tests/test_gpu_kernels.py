@@ -250,7 +250,7 @@ def test_bitpar_prefix_pull_tail_push(msbfs_pkg):
 def test_bitpar_tiled_first_pull(msbfs_pkg, K):
     """The first pull level over static vertex tiles (k_pfx_tiles + big-vertex partial tiles +
     k_bu_wide_finalize, bitpar/tiles.hpp) on a relabelled RMAT-23, 16 words: identical F
-    with the tiles on and off, with and without sparse codes, with a top-down level right after
+    with the tiles on and off, with no / few / most ids coded, with a top-down level right after
     the tiled one (the frontier list comes from the tile bitmap), and equal to the per-group
     distance solver on a sample."""
     m = msbfs_pkg
@@ -258,6 +258,7 @@ def test_bitpar_tiled_first_pull(msbfs_pkg, K):
     g.relabel_by_degree()
     qs = m.QuerySet.random(g.n, K, 16, seed=K)
     runs = {"tiles": {}, "plain": {"tiles": 0}, "nocodes": {"codes": 0},
+            "fewcodes": {"tiles_code_deg": 1}, "manycodes": {"tiles_code_deg": 400},
             "td3": {"dirs": "TBT"}, "td3plain": {"dirs": "TBT", "tiles": 0}}
     out = {}
     for name, tun in runs.items():
