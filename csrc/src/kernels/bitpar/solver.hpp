@@ -193,7 +193,7 @@ class BitparSolver final : public Solver {
     const void* key[2] = {nullptr, nullptr};
   };
   // the tiles of the own vertices (part of nparts; built on first use and cached per graph
-  // buffers; nullptr unless W = 16, or when they do not fit in HBM)
+  // buffers; nullptr for fewer than 8 words, or when they do not fit in HBM)
   const TileSet* pfx_tiles(int W, int part, int nparts, hipStream_t s);
   template <int W>
   int tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t* O, const uint32_t* snap,

@@ -109,13 +109,25 @@ __device__ __forceinline__ TileRound tile_next_round(const PfxTile* tiles, int64
   return tile_first_round(tiles, ntiles, r.t + nwaves);
 }
 
-// 8 group-uniform ballot bytes (lane group k = bits 8k..8k+7, all set or all clear) -> bit k
-__device__ __forceinline__ uint32_t group_bits8(uint64_t m) {
-  m &= 0x8040201008040201ull;
-  m |= m >> 32;
-  m |= m >> 16;
-  m |= m >> 8;
-  return (uint32_t)(m & 0xFFu);
+// bit k = any lane of lane group k (G consecutive lanes) set in the wave mask m (uniform: SALU)
+template <int G>
+__device__ __forceinline__ uint32_t group_any(uint64_t m) {
+  if constexpr (G == 8) {  // OR-fold each byte into its low bit, then gather the 8 bits
+    m |= m >> 4;
+    m |= m >> 2;
+    m |= m >> 1;
+    m &= 0x0101010101010101ull;
+    m |= m >> 7;
+    m |= m >> 14;
+    m |= m >> 28;
+    return (uint32_t)(m & 0xFFu);
+  } else {
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 64 / G; ++k)
+      r |= (uint32_t)(((m >> (k * G)) & ((1ull << G) - 1)) != 0) << k;
+    return r;
+  }
 }
 // OR the bits of a 32-bit tile mask (bit i = vertex v0 + i) into bitmap bm (one lane)
 __device__ __forceinline__ void tile_mask_or(uint32_t* bm, int32_t v0, uint32_t m) {
@@ -135,7 +147,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
     Ctr* ctr, uint32_t* slabF, const uint64_t* zrow, int exp) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, S = 64 / G, VT = kTileVT;
-  static_assert(G == 8 && VPW == 8, "the tile masks take 8 vertices per epilogue pass");
+  static_assert(VPW <= kTileVT && kTileVT % VPW == 0, "whole epilogue passes per tile");
   constexpr int NWV = kTileBlock / 64;
   constexpr int PB = 4;       // rows in flight per lane group and batch
   constexpr int Q = kRoundQ;
@@ -342,21 +354,16 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
             bc.template spill_strided<CR>(cnt, slot);
             nadd = 0;
           }
-          const uint64_t bval = __ballot(valid), bnew = __ballot(anynew);
-          const uint64_t bnf = __ballot(notfull), brnz = __ballot(rnz);
-          // (group-uniform bytes: a group's lanes share validity; OR-ed words -> whole byte)
-          auto grp = [](uint64_t m) {
-            m |= (m >> 1) & 0x7F7F7F7F7F7F7F7Full;
-            m |= (m >> 2) & 0x3F3F3F3F3F3F3F3Full;
-            m |= (m >> 4) & 0x0F0F0F0F0F0F0F0Full;  // bit 8k = OR of byte k
-            return (m & 0x0101010101010101ull) * 0xFFull;
-          };
-          const uint64_t gval = grp(bval), gnew = grp(bnew) & gval;
-          const uint64_t gnf = grp(bnf), gfirst = gnew & ~grp(brnz);
-          m_done |= group_bits8(gval & ~gnf) << p;
-          m_new |= group_bits8(gnew) << p;
-          m_first |= group_bits8(gfirst) << p;
-          const bool g_new = (gnew >> (sub * G)) & 1ull, g_first = (gfirst >> (sub * G)) & 1ull;
+          // per-group flags (a group's lanes share validity; the others OR over its words),
+          // compressed to one bit per group = per vertex of the pass
+          const uint32_t gval = group_any<G>(__ballot(valid));
+          const uint32_t gnew = group_any<G>(__ballot(anynew)) & gval;
+          const uint32_t gnf = group_any<G>(__ballot(notfull));
+          const uint32_t gfirst = gnew & ~group_any<G>(__ballot(rnz));
+          m_done |= (gval & ~gnf) << p;
+          m_new |= gnew << p;
+          m_first |= gfirst << p;
+          const bool g_new = (gnew >> sub) & 1u, g_first = (gfirst >> sub) & 1u;
           const bool leader = valid && slot == 0;
           if (leader && g_new) {
             ++nfc;

@@ -79,7 +79,7 @@ void BitparSolver::prepare(hipStream_t s) {
   constexpr int32_t kPfxH = 14336 * 32;  // (the prefix pull's bound, see level_bu)
   if (g_.rows_sorted && g_.n <= INT32_MAX && tun_.pfx == 2) {
     prefix_lens(kPfxH, s);
-    if (maxW_ == 16) (void)pfx_tiles(16, 0, 1, s);  // (the first pull level's tiles)
+    if (maxW_ >= 8) (void)pfx_tiles(maxW_, 0, 1, s);  // (the first pull level's tiles)
   }
   if (tun_.lean) first_nbr(s);
   (void)code_bound(1.0);
@@ -121,7 +121,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   // the first pull level at level 2 with the prefix pull streams static vertex tiles
   // (bitpar/tiles.hpp) instead of pulling per vertex from active lists
   constexpr int kHubW = 14336, kHubBig = 32768;
-  const bool tiled = !COUNT && W == 16 && tun_.tiles && tun_.pfx == 2 && S.bu_levels == 0 &&
+  const bool tiled = !COUNT && W >= 8 && tun_.tiles && tun_.pfx == 2 && S.bu_levels == 0 &&
                      S.level == 2 && g_.rows_sorted && n <= INT32_MAX &&
                      n > (int64_t)kHubBig * 32 * 4 &&
                      ((S.lazy && S.bu_levels == 0) || (double)S.ev < kFilterFrac * (double)g_.nnz) &&

@@ -61,7 +61,9 @@ __global__ void k_gather_plen(const int32_t* plen, int64_t cnt, int part, int np
 
 const BitparSolver::TileSet* BitparSolver::pfx_tiles(int W, int part, int nparts, hipStream_t s) {
   if (!tiles_ok_ || !tun_.tiles) return nullptr;
-  if (W != 16) return nullptr;  // (k_pfx_tiles: 8 lanes per vertex)
+  // (4 words: no sparse codes, every visited hub's row gathered: RMAT-26 / 256 groups ran
+  // level 2 in 9.7 ms tiled vs 7.4 ms per vertex)
+  if (W < 8) return nullptr;
   for (auto it = tilesets_.begin(); it != tilesets_.end();) {
     TileSet& T = **it;
     if (T.key[0] != (const void*)g_.rowptr || T.key[1] != (const void*)g_.col) {
@@ -144,8 +146,8 @@ template <int W>
 int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t* O,
                              const uint32_t* snap, const uint32_t* codes, int32_t code_from,
                              int rows) {
-  if constexpr (W != 16) {
-    fail("tiled pull: needs 16 words");
+  if constexpr (W < 8) {
+    fail("tiled pull: needs 8 or more words");
   } else {
   const TileSet* T = pfx_tiles(W, S.part, S.nparts, s);
   const Small sm = small();

@@ -246,10 +246,10 @@ def test_bitpar_prefix_pull_tail_push(msbfs_pkg):
     g.close()
 
 
-@pytest.mark.parametrize("K", [1024, 900])
+@pytest.mark.parametrize("K", [1024, 900, 512, 200])
 def test_bitpar_tiled_first_pull(msbfs_pkg, K):
     """The first pull level over static vertex tiles (k_pfx_tiles + big-vertex partial tiles +
-    k_bu_wide_finalize, bitpar/tiles.hpp) on a relabelled RMAT-23, 16 words: identical F
+    k_bu_wide_finalize, bitpar/tiles.hpp) on a relabelled RMAT-23, 16 / 8 / 4 words: identical F
     with the tiles on and off, with no / few / most ids coded, with a top-down level right after
     the tiled one (the frontier list comes from the tile bitmap), and equal to the per-group
     distance solver on a sample."""
