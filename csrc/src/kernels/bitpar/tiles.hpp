@@ -144,7 +144,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
     int nparts, const int64_t* rowptr, const uint64_t* R, uint64_t* O, uint64_t* acc,
     const uint32_t* pvis, const uint32_t* snap, const uint32_t* code, int32_t code_from,
     const uint64_t* alive, const uint64_t* gmask, uint32_t* done, uint32_t* anyvis, uint32_t* fbm,
-    Ctr* ctr, uint32_t* slabF, const uint64_t* zrow, int exp) {
+    Ctr* ctr, uint32_t* slabF, const uint64_t* zrow) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, S = 64 / G, VT = kTileVT;
   static_assert(VPW <= kTileVT && kTileVT % VPW == 0, "whole epilogue passes per tile");
@@ -225,8 +225,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
 #pragma unroll
       for (int i = 0; i < kCodeSlots; ++i) {
         const int g = coded ? code_g(cdc[q], i) : -1;
-        if (!(exp & 2))  // (timing experiment: no code ORs)
-          atomicOr(&y[g >= 0 ? vl * W + (g >> 6) : dummy], g >= 0 ? 1ull << (g & 63) : 0ull);
+        atomicOr(&y[g >= 0 ? vl * W + (g >> 6) : dummy], g >= 0 ? 1ull << (g & 63) : 0ull);
       }
       pkc[q] = coded ? kPentNone : pkc[q];
     }
@@ -240,7 +239,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
       c += __popcll(m);
     }
     __builtin_amdgcn_wave_barrier();
-    for (int b = 0; b < ((exp & 4) ? 0 : c); b += PB * S) {  // (exp 4: no row gathers)
+    for (int b = 0; b < c; b += PB * S) {
       uint32_t uu[PB];
 #pragma unroll
       for (int q = 0; q < PB; ++q) {
@@ -264,7 +263,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
       }
     }
     __builtin_amdgcn_wave_barrier();
-    if (rc.e + kRound >= rc.e1 && !(exp & 8)) {  // last round of the tile (exp 8: no epilogue)
+    if (rc.e + kRound >= rc.e1) {  // last round of the tile
       const int32_t v0 = uni32(tiles[rc.t].v0);
       const int32_t nvf = uni32(tiles[rc.t].nv);
       if (nvf & kTilePartial) {
@@ -349,7 +348,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
             rnz |= r.w[j] != 0;
           }
           if (valid) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
-          if (!(exp & 16)) bc.add(nw);  // (exp 16: no counting)
+          bc.add(nw);
           if (++nadd == (1 << 4) - 1) {
             bc.template spill_strided<CR>(cnt, slot);
             nadd = 0;

@@ -42,7 +42,6 @@ void Tuning::set(const std::string& key, const std::string& v) {
     if (batch < 1 || batch > 64) fail("tuning: batch must be in [1, 64]");
   } else if (key == "bu_max") bu_max = (int64_t)to_num(key, v);
   else if (key == "tiles") tiles = (int)to_num(key, v);
-  else if (key == "tiles_exp") tiles_exp = (int)to_num(key, v);
   else if (key == "tiles_code_deg") tiles_code_deg = to_num(key, v);
   else if (key == "dirs") {
     for (char c : v)
@@ -50,7 +49,7 @@ void Tuning::set(const std::string& key, const std::string& v) {
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_exp tiles_code_deg dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg dirs)");
   }
 }
 

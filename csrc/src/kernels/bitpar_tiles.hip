@@ -160,8 +160,7 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
       T->tiles.as<PfxTile>(), T->ntiles, T->pent.as<uint32_t>(), S.nparts, g_.rowptr, R, O,
       acc_[S.ac].as<uint64_t>(), pvis, snap, codes, codes ? code_from : INT32_MAX, alive,
       sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), fbm_tile_.as<uint32_t>(),
-      ctr_.as<Ctr>(), slabF<W>(rows), zrow_.as<uint64_t>(),
-      tun_.tiles_exp);
+      ctr_.as<Ctr>(), slabF<W>(rows), zrow_.as<uint64_t>());
   MSBFS_HIP_CHECK(hipGetLastError());
   rows += grid;
   if (T->nbig) {
