@@ -288,6 +288,7 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
     const uint64_t agree = comm->allreduce_min_u64((hybrid_local ? 2u : 0u) | (want_coded ? 1u : 0u));
     const bool hybrid = agree >= 2 && same_ids;
     const bool hcoded = hybrid && (agree & 1u);
+    if (hybrid) solver->prepare_hybrid(me, P, stream);  // (preprocessing: phase A's tables)
     if (a.dist == "hybrid" && !hybrid && me == 0)
       fprintf(stderr,
               "msbfs: --dist hybrid needs --algo bitpar, <= %d ranks and K <= one pass on every "

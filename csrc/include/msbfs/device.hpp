@@ -136,6 +136,12 @@ class Solver {
   // Build graph-derived tables and worst-case scratch now (before a timed region) instead of on
   // the first run.
   virtual void prepare(hipStream_t stream) { (void)stream; }
+  // The same for hybrid phase A as part `part` of `nparts` (its own vertices' tables)
+  virtual void prepare_hybrid(int part, int nparts, hipStream_t stream) {
+    (void)part;
+    (void)nparts;
+    (void)stream;
+  }
   // Algorithm tuning, "key=value,key=value" (bit-parallel solver: see bp::Tuning in
   // kernels/bitpar/solver.hpp). Unknown keys are errors; solvers without tuning reject any.
   virtual void tune(const std::string& spec) {

@@ -113,6 +113,8 @@ int msbfs_solver_tune(msbfs_solver s, const char* spec);
 /* Build graph-derived tables and worst-case scratch now instead of in the first run (the CLI
  * calls it during preprocessing; optional). */
 int msbfs_solver_prepare(msbfs_solver s, void* stream);
+/* The same for the hybrid phase A of rank `part` of `nparts` (call it before timing hybrid runs). */
+int msbfs_solver_prepare_hybrid(msbfs_solver s, int part, int nparts, void* stream);
 /* F[k] for k in [0,K); edges2 (nullable) = per-group sum of reached degrees (2x the Graph500
  * traversed-edge count). stream = hipStream_t or NULL for the null stream. */
 int msbfs_solver_run(msbfs_solver s, int64_t K, const int64_t* qoff, const int32_t* qids,

@@ -384,6 +384,14 @@ int msbfs_solver_prepare(msbfs_solver s, void* stream) {
   });
 }
 
+int msbfs_solver_prepare_hybrid(msbfs_solver s, int part, int nparts, void* stream) {
+  return guard([&] {
+    if (nparts < 1 || part < 0 || part >= nparts) msbfs::fail("prepare_hybrid: bad part index");
+    MSBFS_HIP_CHECK(hipSetDevice(s->graph->g.device));
+    s->impl->prepare_hybrid(part, nparts, (hipStream_t)stream);
+  });
+}
+
 int msbfs_solver_tune(msbfs_solver s, const char* spec) {
   return guard([&] {
     if (!spec) msbfs::fail("msbfs_solver_tune: null spec");

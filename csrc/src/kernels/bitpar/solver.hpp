@@ -98,6 +98,7 @@ class BitparSolver final : public Solver {
   int64_t pass_groups() const override { return 64 * (int64_t)std::min(maxW_, opt.max_words); }
   // graph-derived tables and worst-case scratch, built before any timed run (bitpar_pull.hip)
   void prepare(hipStream_t s) override;
+  void prepare_hybrid(int part, int nparts, hipStream_t s) override;
 
   int64_t hybrid_max_groups() const override { return 64 * (int64_t)maxW_; }
   void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,

@@ -139,6 +139,13 @@ const BitparSolver::TileSet* BitparSolver::pfx_tiles(int W, int part, int nparts
   return &T;
 }
 
+// phase A of part `part` of `nparts` pulls its level 2 over the tiles of its own vertices
+void BitparSolver::prepare_hybrid(int part, int nparts, hipStream_t s) {
+  if (g_.rows_sorted && g_.n <= INT32_MAX && tun_.pfx == 2 && maxW_ >= 8)
+    (void)pfx_tiles(maxW_, part, nparts, s);
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+}
+
 // The first pull level of a batch over the tiles (see level_bu: called after the tail push).
 // Returns the slab rows it wrote; leaves the next active lists in act_[1] / actw_[1] and the
 // frontier in fbm_tile_ (S.fl_bitmap).

@@ -60,6 +60,11 @@ class Solver:
         native.check(native.lib().msbfs_solver_prepare(self._h, C.c_void_p(stream) if stream
                                                        else None))
 
+    def prepare_hybrid(self, part: int, nparts: int, stream: Optional[int] = None) -> None:
+        """prepare() for the hybrid phase A of rank `part` of `nparts` (its own vertices)."""
+        native.check(native.lib().msbfs_solver_prepare_hybrid(
+            self._h, int(part), int(nparts), C.c_void_p(stream) if stream else None))
+
     def tune(self, tuning) -> None:
         spec = tuning if isinstance(tuning, str) else ",".join(
             f"{k}={v}" for k, v in dict(tuning).items())

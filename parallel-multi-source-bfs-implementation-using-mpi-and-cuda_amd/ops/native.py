@@ -100,6 +100,7 @@ def _sig(lib):
         "msbfs_solver_set_options": (C.c_int, [vp, P(Options)]),
         "msbfs_solver_tune": (C.c_int, [vp, C.c_char_p]),
         "msbfs_solver_prepare": (C.c_int, [vp, vp]),
+        "msbfs_solver_prepare_hybrid": (C.c_int, [vp, C.c_int, C.c_int, vp]),
         "msbfs_solver_run": (C.c_int, [vp, C.c_int64, i64p, i32p, i64p, i64p, P(Stats), vp]),
         "msbfs_solver_free": (None, [vp]),
         "msbfs_solver_levels": (C.c_int64, [vp, P(Level), C.c_int64]),

