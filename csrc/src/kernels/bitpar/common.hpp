@@ -252,6 +252,34 @@ struct BitCounter {
       for (int d = 0; d < D; ++d) c[j][d] = 0;
     }
   }
+  // spill_strided with 32-bit halves (~12 instead of ~21 VALU per set counter bit: the
+  // first pull level sets about half the bits of every word between two spills)
+  template <int STRIDE>
+  __device__ __forceinline__ void spill_strided32(uint32_t* f, int slot) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t sl[D], any = 0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          sl[d] = (uint32_t)(c[j][d] >> (32 * h));
+          any |= sl[d];
+        }
+        uint32_t* row = f + (slot * VW + j) * STRIDE + 32 * h;
+        while (any) {
+          const int b = __ffs(any) - 1;
+          any &= any - 1;
+          uint32_t v = 0;
+#pragma unroll
+          for (int d = 0; d < D; ++d) v |= ((sl[d] >> b) & 1u) << d;
+          atomicAdd(&row[b], v);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) c[j][d] = 0;
+    }
+  }
 };
 
 // Gate of a level of a device-driven pull batch (BitparSolver::bu_batch): level i reads counter

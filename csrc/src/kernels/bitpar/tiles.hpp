@@ -218,14 +218,18 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
       __builtin_amdgcn_wave_barrier();
     }
     // ---- round r: sparse codes straight into the accumulator rows (idle slots: dummy word)
+    // (32-bit halves of the rows: one shift per bit; an idle slot ORs 0 into its lane's dummy)
+    uint32_t* y32 = reinterpret_cast<uint32_t*>(y);
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const bool coded = pkc[q] != kPentNone && cdc[q] != kDenseCode;
-      const int vl = (int)(pkc[q] >> kPentUBits);
+      const uint32_t vrow = (pkc[q] >> kPentUBits) * (2 * W);
+      const uint32_t nset = cdc[q] >> 30;
 #pragma unroll
       for (int i = 0; i < kCodeSlots; ++i) {
-        const int g = coded ? code_g(cdc[q], i) : -1;
-        atomicOr(&y[g >= 0 ? vl * W + (g >> 6) : dummy], g >= 0 ? 1ull << (g & 63) : 0ull);
+        const uint32_t g = (cdc[q] >> (10 * i)) & 1023u;
+        const bool on = coded && (uint32_t)i < nset;
+        atomicOr(&y32[on ? vrow + (g >> 5) : 2 * dummy], 1u << (g & 31));
       }
       pkc[q] = coded ? kPentNone : pkc[q];
     }
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           if (valid) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
           bc.add(nw);
           if (++nadd == (1 << 4) - 1) {
-            bc.template spill_strided<CR>(cnt, slot);
+            bc.template spill_strided32<CR>(cnt, slot);
             nadd = 0;
           }
           // per-group flags (a group's lanes share validity; the others OR over its words),
@@ -394,7 +398,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
   block_sum_add32(nfc, &ctr->fl2.v, scratch32);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
-  bc.template spill_strided<CR>(cnt, slot);
+  bc.template spill_strided32<CR>(cnt, slot);
   __syncthreads();
   uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
   for (int i = threadIdx.x; i < 64 * W; i += kTileBlock) row[i] = cnt[i + (i >> 6)];
