@@ -172,9 +172,9 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
   __syncthreads();
   unsigned long long ef = 0, ev = 0;
   uint32_t nfc = 0;
-  // 4 slices: a spill (one LDS add per set counter bit, ~100 per lane at level 2) every 15
-  // passes (3 slices: every 7; 5 do not fit the 128 VGPRs of a 1024-thread block)
-  BitCounter<VW, 4> bc;
+  // 5 slices: a spill (one LDS add per set counter bit, ~100 per lane at level 2) every 31
+  // passes (6 slices do not fit the 128 VGPRs of a 1024-thread block at 16 words)
+  BitCounter<VW, 5> bc;
   bc.zero();
   int nadd = 0;
   const int64_t nwaves = (int64_t)gridDim.x * NWV;
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           }
           if (valid) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
           bc.add(nw);
-          if (++nadd == (1 << 4) - 1) {
+          if (++nadd == (1 << 5) - 1) {
             bc.template spill_strided32<CR>(cnt, slot);
             nadd = 0;
           }
