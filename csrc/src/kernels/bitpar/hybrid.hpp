@@ -59,22 +59,38 @@ __device__ __forceinline__ int code_seg(const CodeSegs& cs, int nseg, int64_t c)
 
 // send[cnt*wbeg[j] + i*nw_j + (w-wbeg[j])] = vis[v*W + w], v = part + i*nparts: destination-major
 // (rows of deg-0 vertices may be stale, see k_zero_src_rows: they are sent as zeros; phase C
-// never reads them either)
+// never reads them either). G lanes per vertex (the row layout): one degree test and one 8*VW-byte
+// row load per lane; a destination's words of consecutive vertices are contiguous, so the lanes
+// of one slot store adjacent runs (one word per thread with a 64-bit divide and a degree test per
+// word took 0.32 ms per rank at 8 ranks on RMAT-26)
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, const int64_t* rowptr,
                                                        int part, int nparts, int64_t cnt, int wt,
                                                        WordSplit ws, uint64_t* send) {
-  const int64_t total = cnt * wt;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
-    const int64_t i = t / wt;
-    const int w = (int)(t - i * wt);
-    const int64_t v = part + i * nparts;
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
+  // destination of each of this lane's words (fixed for the whole kernel)
+  int dj[VW], doff[VW], dnw[VW];
+#pragma unroll
+  for (int k = 0; k < VW; ++k) {
+    const int w = slot * VW + k;
     int j = 0;
-    while (w >= ws.b[j + 1]) ++j;
-    const int nw = ws.b[j + 1] - ws.b[j];
+    if (w < wt)
+      while (w >= ws.b[j + 1]) ++j;  // (w < wt = ws.b[nparts]: ends at a real part)
+    dj[k] = j;
+    dnw[k] = ws.b[j + 1] - ws.b[j];
+    doff[k] = w - ws.b[j];
+  }
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < cnt; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t i = tb + wv * VPW + sub;
+    if (i >= cnt) continue;
+    const int64_t v = part + i * nparts;
     const bool deg0 = rowptr[v + 1] == rowptr[v];
-    send[cnt * ws.b[j] + i * nw + (w - ws.b[j])] = deg0 ? 0ull : vis[v * W + w];
+    const V<VW> r = deg0 ? vzero<VW>() : ldv<VW>(vis + v * W + slot * VW);
+#pragma unroll
+    for (int k = 0; k < VW; ++k)
+      if (slot * VW + k < wt) send[cnt * ws.b[dj[k]] + i * dnw[k] + doff[k]] = r.w[k];
   }
 }
 

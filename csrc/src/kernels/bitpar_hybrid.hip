@@ -98,7 +98,7 @@ void BitparSolver::code_send(const uint64_t* vis, uint64_t* staging, int64_t cnt
   for (int j = 0; j < nparts; ++j) coded_len[j] = 0;
   if (c == 0) return;
   const CodeWs w = code_ws(c);
-  k_pack_words<W><<<grid_for(cnt * ws.b[nparts], kBlock, 8192), kBlock, 0, s>>>(
+  k_pack_words<W><<<grid_for(cnt, Lay<W>::TILE, 8192), kBlock, 0, s>>>(
       vis, g_.rowptr, part, nparts, cnt, ws.b[nparts], ws, staging);
   MSBFS_HIP_CHECK(hipGetLastError());
   const int gc = grid_for((c + kCodeCPW - 1) / kCodeCPW * 64, kBlock, 1 << 20);
@@ -175,7 +175,7 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
     code_send<W>(vis_[S.cur].as<uint64_t>(), vis_[S.cur ^ 1].as<uint64_t>(), S.cnt, part,
                  nparts, wbeg, send, coded_len, s);
   } else if (S.cnt > 0) {
-    k_pack_words<W><<<grid_for(S.cnt * wt, kBlock, 8192), kBlock, 0, s>>>(
+    k_pack_words<W><<<grid_for(S.cnt, Lay<W>::TILE, 8192), kBlock, 0, s>>>(
         vis_[S.cur].as<uint64_t>(), g_.rowptr, part, nparts, S.cnt, wt, ws, send);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
