@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kBlock) void k_push_tail(
       const int32_t v = col[k];
       if (nparts > 1 && (pmask ? ((uint32_t)v & pmask) != (uint32_t)part : v % nparts != part))
         continue;
-      if (is_done(done, v)) continue;
+      if (done && is_done(done, v)) continue;  // (nullptr: the consumer clears done rows too)
       if (c != kDenseCode) {
         for (int i = 0; i < kCodeSlots; ++i) {
           const int g = code_g(c, i);
@@ -923,7 +923,11 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     uint32_t deg = 0;
     if (valid) {
       v = wl[idx];
-      if (fbm && is_done(done, v)) valid = false;
+      if (fbm && is_done(done, v)) {
+        // (the tiled level's tail push also pushes into done vertices: leave their acc row clean)
+        stv<VW>(acc + (int64_t)v * W + slot * VW, vzero<VW>());
+        valid = false;
+      }
     }
     if (valid) {
       const int64_t vo = (int64_t)v * W + slot * VW;

@@ -317,8 +317,9 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
             const int64_t vo = (int64_t)(v0 + i * nparts) * W + slot * VW;
             rr[k] = ((bvis >> i) & 1ull) ? ldv<VW>(R + vo) : vzero<VW>();
             // bits pushed by k_push_tail (no stamps: the level's acc rows are all-zero but
-            // the pushed ones, and a tile's rows are one contiguous run)
-            pa[k] = ((bok >> i) & 1ull) ? ldv<VW>(acc + vo) : vzero<VW>();
+            // the pushed ones, and a tile's rows are one contiguous run; the push skips no done
+            // vertex either, so every vertex of the tile reads and clears its row)
+            pa[k] = i < nv ? ldv<VW>(acc + vo) : vzero<VW>();
           }
 #pragma unroll
         for (int k = 0; k < NH; ++k) {
@@ -332,12 +333,13 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           V<VW> r = vzero<VW>(), a = vzero<VW>();
           if (valid) {
             r = rr[k];
+#pragma unroll
+            for (int j = 0; j < VW; ++j) a.w[j] = y[i * W + slot * VW + j] | pa[k].w[j];
+          }
+          {
             bool pushed = false;
 #pragma unroll
-            for (int j = 0; j < VW; ++j) {
-              a.w[j] = y[i * W + slot * VW + j] | pa[k].w[j];
-              pushed |= pa[k].w[j] != 0;
-            }
+            for (int j = 0; j < VW; ++j) pushed |= pa[k].w[j] != 0;
             if (pushed) stv<VW>(acc + (int64_t)v * W + slot * VW, vzero<VW>());
           }
           V<VW> nw, nvr;

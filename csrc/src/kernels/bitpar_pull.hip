@@ -205,7 +205,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     ++epoch_;
     k_push_tail<W><<<grid_for(S.nf * 64, kBlock, 8192), kBlock, 0, s>>>(
         fl_[S.fc].as<int32_t>(), S.nf, kPfxH, g_.rowptr, g_.col, R, codes, code_from,
-        done_.as<uint32_t>(), S.part, S.nparts, acc_[S.ac].as<uint64_t>(),
+        tiled ? nullptr : done_.as<uint32_t>(), S.part, S.nparts, acc_[S.ac].as<uint64_t>(),
         tiled ? nullptr : stamp_.as<int32_t>(), epoch_);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
