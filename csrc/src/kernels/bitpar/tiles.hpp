@@ -24,7 +24,11 @@
 // (several rows in flight per group) and OR-ed into the accumulator rows. The epilogue is the
 // narrow pull's (new bits, row store, counters, done / any-visited bits) minus the list
 // queues: the frontier goes into a bitmap (materialised as a list only if a top-down level
-// follows) and the next active lists come from one k_build_active pass after the level.
+// follows) and the next active lists come from one k_build_active pass after the level. The
+// tail push before it (k_push_tail) runs without stamps or done tests: the level's acc rows are
+// all-zero but the pushed ones, and every tile vertex (and big vertex) reads and clears its own.
+// Used from 8 words on (4 words: no sparse codes, slower than the per-vertex pulls).
+// RMAT-26 / 1024 groups: level 2 14.9 -> 12.3-12.5 ms (profiles/rmat26_tiles_counters.md).
 #pragma once
 
 #include "common.hpp"
@@ -53,8 +57,8 @@ constexpr int kTileHubW = 14336;    // hub bitmap words (ids < 458752, the prefi
 constexpr int kTileVT = 32;
 constexpr int kVertexWeight = kTileWeight / kTileVT;
 
-// pent for the vertices of normal tiles (one wave per tile: a wave prefix sum over the <= VT
-// prefix lengths) and of the big vertices (one wave per vertex, vl = 0)
+// pent for the vertices of normal tiles (one wave per tile, the vertices one after another) and
+// for the partial tiles of big vertices (their slice of the row prefix, vl = 0)
 __global__ __launch_bounds__(256) void k_fill_pent(const PfxTile* tiles, int64_t ntiles,
                                                    int nparts, const int64_t* rowptr,
                                                    const int32_t* col, const int32_t* plen,
