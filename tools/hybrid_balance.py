@@ -11,6 +11,7 @@ prints every rank's phase C for each ordering:
   shuffle  random permutations
   snake    groups sorted by a lateness key, dealt to the ranks in snake order (balanced mix)
   cluster  the same sorted order, contiguous (late groups together)
+  pair     sorted order, the last rank holding the 64 latest and the 64 earliest groups
 
 Lateness key of a group = the smallest internal (degree-descending) id among its sources, i.e.
 the degree rank of its best-connected source: a group whose every source has low degree reaches
@@ -52,6 +53,7 @@ def main():
     ap.add_argument("--group-size", type=int, default=16)
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--orders", nargs="+", default=None, help="subset of the orderings to run")
     args = ap.parse_args()
 
     import msbfs
@@ -66,11 +68,14 @@ def main():
     order = np.argsort(key, kind="stable")
     rng = np.random.default_rng(1)
     plans = {"orig": np.arange(K), "shuffle1": rng.permutation(K), "shuffle2": rng.permutation(K),
-             "snake": snake(order, K, N, wbeg), "cluster": order}
+             "snake": snake(order, K, N, wbeg), "cluster": order,
+             "pair": np.concatenate([order[64:K - 64], order[:64], order[K - 64:]])}
     with msbfs.Solver(g, "bitpar", max_groups=K) as s:
         ref = s.run(qs)
         H.emulate_ranks(s, qs, N)  # warm
         for name, perm in plans.items():
+            if args.orders and name not in args.orders:
+                continue
             sub = qs.subset(perm)
             best = None
             for _ in range(args.reps):
