@@ -77,6 +77,8 @@ def main() -> int:
                          "(untimed, max over ranks) and time the fastest")
     ap.add_argument("--relabel", type=int, default=1,
                     help="renumber vertices by descending degree after generation (preprocessing)")
+    ap.add_argument("--test-corrupt", default="",
+                    help=argparse.SUPPRESS)  # tests only: candidate whose F is falsified
     args = ap.parse_args()
     # --gpus N without a launcher: start the N ranks ourselves (one process per GPU over RCCL),
     # before this process touches the GPU, and hand back the child's exit status
@@ -97,6 +99,13 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     ctx = D.init_from_env(backend=args.backend, use_gpu=True)
     dev = ctx.device
+    # which GPU every rank drives: one per rank under RCCL (it refuses duplicates anyway)
+    devices = D.allgather_int(torch.cuda.current_device(), ctx)
+    if ctx.backend == "nccl" and ctx.world > 1 and len(set(devices)) != len(devices):
+        print(f"bench: ranks share GPUs under RCCL: {devices}", file=sys.stderr)
+        return 2
+    import torch.distributed as tdist
+    pg_size = tdist.get_world_size() if ctx.distributed and tdist.is_initialized() else 1
     t_setup = time.perf_counter()
     g = msbfs.DeviceGraph.rmat(args.scale, args.edgefactor, args.seed, device=dev)
     relabelled = False
@@ -123,24 +132,43 @@ def main() -> int:
     candidates = {"auto": ["roundrobin", "hybrid", "hybrid-coded"] if hybrid_ok else ["roundrobin"],
                   "roundrobin": ["roundrobin"], "hybrid": ["hybrid"],
                   "hybrid-coded": ["hybrid-coded"]}[args.dist]
-    plans = {}
+    plans, cand_err = {}, {}
     for m in candidates:
-        if m.startswith("hybrid"):
-            runner = H.HybridRunner(solver, qs.K, ctx, coded=m == "hybrid-coded")
-            plans[m] = (runner, runner.idx)
-        else:
-            rr = D.round_robin(qs.K, ctx.rank, ctx.world)
-            plans[m] = (qs.subset(rr), rr)
+        err = ""
+        try:
+            if m.startswith("hybrid"):
+                runner = H.HybridRunner(solver, qs.K, ctx, coded=m == "hybrid-coded")
+                plans[m] = (runner, runner.idx)
+            else:
+                rr = D.round_robin(qs.K, ctx.rank, ctx.world)
+                plans[m] = (qs.subset(rr), rr)
+        except Exception as e:  # noqa: BLE001 (a candidate that cannot be set up is dropped)
+            err = f"{type(e).__name__}: {e}"[:240]
+        if not D.agree_ok(not err, ctx):
+            cand_err[m] = err or "setup failed on another rank"
+            plans.pop(m, None)
+    candidates = [m for m in candidates if m in plans]
+    if "roundrobin" not in plans and args.dist in ("auto", "roundrobin"):
+        print(f"bench: round robin could not be set up: {cand_err}", file=sys.stderr)
+        return 3
     torch.cuda.synchronize(dev)
     setup_s = time.perf_counter() - t_setup
 
-    def step(m):
+    def step(m, checked=False):
         runner = plans[m][0]
         if m.startswith("hybrid"):
-            res = runner.run(qs)
-            return res.F, res.stats
-        r = solver.run(runner)  # round robin: the rank's query subset
-        return r.F, r.stats
+            res = runner.run(qs, checked=checked)
+            F, st = res.F, res.stats
+        elif checked:
+            r = D.checked(lambda: solver.run(runner), ctx, "round robin")
+            F, st = r.F, r.stats
+        else:
+            r = solver.run(runner)  # round robin: the rank's query subset
+            F, st = r.F, r.stats
+        if args.test_corrupt == m and len(F):  # (tests: a candidate with a wrong answer)
+            F = F.copy()
+            F[0] += 1
+        return F, st
 
     # untimed: TEPS numerator (traversed edges per group) — also the first warm-up pass
     rr_idx = D.round_robin(qs.K, ctx.rank, ctx.world)
@@ -151,21 +179,24 @@ def main() -> int:
     F_ref = D.gather_F(r0.F, rr_idx, qs.K, ctx)
     # Each candidate runs twice and keeps its faster time: the first run of a decomposition can
     # carry one-time costs (e.g. RCCL setting up the all-to-all's peer connections) that would
-    # otherwise decide the choice.
-    cand_ms = {}
-    for m in candidates:
-        for rep in range(2 if ctx.distributed else 1):
-            D.barrier(ctx)
-            torch.cuda.synchronize(dev)
-            t = time.perf_counter()
-            Fm, _ = step(m)
-            torch.cuda.synchronize(dev)
-            ms = D.allreduce_max(time.perf_counter() - t, ctx) * 1e3
-            cand_ms[m] = min(cand_ms.get(m, ms), ms)
-            Fg = D.gather_F(Fm, plans[m][1], qs.K, ctx)  # identical on every rank
-            if not np.array_equal(Fg, F_ref):
-                print(f"rank {ctx.rank}: {m} F differs from the round-robin pass", file=sys.stderr)
-                return 3
+    # otherwise decide the choice. Round robin goes first; a candidate that raises (on any rank)
+    # or whose gathered F differs from the untimed round-robin pass is excluded (every rank
+    # decides alike) and reported in candidate_errors; only round robin failing ends the run.
+
+    def run_gathered(m):
+        Fm, st = step(m, checked=True)
+        return D.gather_F(Fm, plans[m][1], qs.K, ctx), st  # identical on every rank
+
+    cand_ms, errs = D.evaluate_candidates(candidates, run_gathered, F_ref, ctx,
+                                          reps=2 if ctx.distributed else 1,
+                                          sync=lambda: torch.cuda.synchronize(dev))
+    cand_err.update(errs)
+    for m, e in errs.items():
+        if ctx.rank == 0:
+            print(f"bench: candidate {m} excluded: {e}", file=sys.stderr)
+    if "roundrobin" in cand_err or not cand_ms:
+        print(f"rank {ctx.rank}: no verified decomposition: {cand_err}", file=sys.stderr)
+        return 3
     mode = min(cand_ms, key=cand_ms.get)
     local_idx = plans[mode][1]
     for _ in range(max(0, args.warmup)):
@@ -186,6 +217,15 @@ def main() -> int:
     dt = D.allreduce_max(dt, ctx)  # slowest rank
     ms = dt / max(1, args.steps) * 1e3
     trace = solver.level_trace()  # last timed step: per-level direction and host wall time
+    # hybrid: per-phase wall ms of the last timed step, max over ranks, and the all-to-all rate
+    phases = {}
+    if mode.startswith("hybrid"):
+        for key in ("phase_a_wall_ms", "exchange_ms", "phase_c_wall_ms", "phase_a_ms",
+                    "phase_c_ms"):
+            phases[key] = round(D.allreduce_max(float(stats.get(key) or 0.0), ctx), 3)
+        sent = D.allreduce_max(float(stats.get("sent_bytes", 0)), ctx)
+        xms = phases.get("exchange_ms") or 0.0
+        phases["alltoall_GBps_per_rank"] = round(sent / (xms * 1e6), 1) if xms > 0 else None
     # ---- untimed self-check of the timed result: the last timed step's F (all ranks, gathered)
     # equals the untimed pass, and the first groups of every rank equal the per-group distance
     # solver's F (an independent algorithm: one int32 distance per vertex, main.cu:40-89)
@@ -249,6 +289,9 @@ def main() -> int:
                 "level_ms": [round(t["ms"], 3) for t in trace],
                 "setup_s": round(setup_s, 3), "relabel": relabelled,
                 "candidates_ms": {k: round(v, 3) for k, v in cand_ms.items()},
+                "candidate_errors": cand_err,
+                "devices": devices, "process_group_size": pg_size, "backend": ctx.backend,
+                **({"phases": phases} if phases else {}),
                 "timed_F_equals_untimed": True,
                 "verified_groups_vs_dist_solver": verified,
                 **({"verify_skipped": verify_err} if verify_err else {}),

@@ -46,6 +46,8 @@ struct Args {
   int threads = 0;
   int repeat = 1;
   int spmd = 0;
+  int max_words = 0;    // bit-parallel: at most 64*max_words groups per solver pass (0: all fit)
+  int async_slots = 0;  // asynchronous MIN slots before a drain (0: Comm::kAsyncSlots; tests)
   bool cache = false, json = false, sort_rows = false, relabel = true;
 };
 
@@ -145,19 +147,41 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
       }
       if (!a.graph.size()) a.graph = a.gen;
     } else {
-      int64_t hdr[2] = {0, 0};
+      // rank 0 reads the file (main.cu:237-239). GPU runs build the CSR on the device straight
+      // from the mapped edge list (device_graph_from_edge_file); --cache keeps the host build,
+      // whose sidecar skips parsing altogether on the next run.
+      int64_t hdr[3] = {0, 0, 0};  // n, m, CSR already on rank 0's device
       if (comm->rank() == 0) {
         try {
-          hg = load_graph(a.graph, a.cache, a.threads);
+          if (!cpu && !a.cache) {
+            device_graph_from_edge_file(dg, a.graph, stream);
+            hdr[0] = dg.n;
+            hdr[1] = dg.m;
+            hdr[2] = 1;
+          } else {
+            hg = load_graph(a.graph, a.cache, a.threads);
+            hdr[0] = hg.n;
+            hdr[1] = hg.m;
+          }
         } catch (const Error& e) {
           fprintf(stderr, "%s\n", e.what());  // "Could not open graph file %s" (main.cu:97)
           comm->abort(EXIT_FAILURE);
         }
-        hdr[0] = hg.n;
-        hdr[1] = hg.m;
       }
       comm->bcast_host(hdr, sizeof(hdr), 0);
       const int64_t n = hdr[0], m = hdr[1];
+      const bool on_device = hdr[2] != 0;
+      if (on_device && comm->rank() == 0 && !comm->device_collectives() && comm->size() > 1) {
+        // host collectives: the other ranks get the device-built CSR through host memory
+        hg.n = n;
+        hg.m = m;
+        hg.rowptr.resize(n + 1);
+        hg.col.resize(2 * m);
+        MSBFS_HIP_CHECK(hipMemcpy(hg.rowptr.data(), dg.rowptr, (n + 1) * sizeof(int64_t),
+                                  hipMemcpyDeviceToHost));
+        MSBFS_HIP_CHECK(hipMemcpy(hg.col.data(), dg.col, 2 * m * sizeof(int32_t),
+                                  hipMemcpyDeviceToHost));
+      }
       if (cpu) {
         if (comm->rank() != 0) {
           hg.n = n;
@@ -168,9 +192,9 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
         comm->bcast_host(hg.rowptr.data(), (n + 1) * sizeof(int64_t), 0);
         comm->bcast_host(hg.col.data(), 2 * m * sizeof(int32_t), 0);
       } else if (comm->device_collectives()) {
-        // upload once on rank 0, then HBM -> HBM broadcast over xGMI
+        // upload once on rank 0 (or built there), then HBM -> HBM broadcast over xGMI
         if (comm->rank() == 0) {
-          device_graph_from_host(dg, n, hg.rowptr.data(), hg.col.data(), stream);
+          if (!on_device) device_graph_from_host(dg, n, hg.rowptr.data(), hg.col.data(), stream);
           hg = HostCsr();
         } else {
           dg.n = n;
@@ -192,9 +216,12 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
           hg.rowptr.resize(n + 1);
           hg.col.resize(2 * m);
         }
-        comm->bcast_host(hg.rowptr.data(), (n + 1) * sizeof(int64_t), 0);
-        comm->bcast_host(hg.col.data(), 2 * m * sizeof(int32_t), 0);
-        device_graph_from_host(dg, n, hg.rowptr.data(), hg.col.data(), stream);
+        if (comm->size() > 1) {
+          comm->bcast_host(hg.rowptr.data(), (n + 1) * sizeof(int64_t), 0);
+          comm->bcast_host(hg.col.data(), 2 * m * sizeof(int32_t), 0);
+        }
+        if (!(on_device && comm->rank() == 0))
+          device_graph_from_host(dg, n, hg.rowptr.data(), hg.col.data(), stream);
         hg = HostCsr();
       }
     }
@@ -272,6 +299,7 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
         if (dalgo == 3) solver->opt.force_dir = 1;
       }
       if (a.json) solver->opt.count_edges = true;
+      if (a.max_words > 0) solver->opt.max_words = a.max_words;
       if (!a.tune.empty()) solver->tune(a.tune);
       solver->prepare(stream);  // graph-derived tables: preprocessing, not computation
       MSBFS_HIP_CHECK(hipDeviceSynchronize());
@@ -367,7 +395,12 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
                                                     : std::max<int64_t>(1, solver->pass_groups());
     const int npass_local = nlocal ? (int)(1 + (nlocal - 1) / pass) : 0;
     const int npass = hybrid ? 1 : (int)comm->allreduce_max_f64((double)npass_local);
-    if (npass > Comm::kAsyncSlots) fail("too many solver passes for the asynchronous reduction");
+    // more passes than asynchronous slots (small solver widths on huge graphs): the slots are
+    // drained every kAsyncSlots passes and folded into the running minimum (every rank drains at
+    // the same pass, since npass is agreed on)
+    int nslots = std::min(npass, (int)Comm::kAsyncSlots);
+    if (a.async_slots > 0) nslots = std::min(nslots, a.async_slots);
+    nslots = std::max(nslots, 1);
     comm->reserve_device_scratch((size_t)std::max<int64_t>(hout.size(), a.json ? K : 0) * 8);
     int qbits = 1;
     while ((int64_t(1) << qbits) <= K) ++qbits;
@@ -382,7 +415,7 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
         key = std::min(key, 1 + (((uint64_t)F[i] << qbits) | (uint64_t)local_to_global[i]));
       return key;
     };
-    std::vector<uint64_t> keys(std::max(npass, 1));
+    std::vector<uint64_t> keys(nslots);
     for (int rep = 0; rep < a.repeat; ++rep) {
       comm->barrier();
       trace::Range range_compute("computation");
@@ -429,6 +462,14 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
       // ONE packed min-reduce of 1 + (F << qbits | q) per pass keeps the lowest-index tie-break
       // (main.cu:391-396); a rank whose F would not fit next to the query index sends 0, so
       // every rank sees 0 and takes the two-pass fallback together
+      uint64_t key = NONE;
+      int pending = 0;  // slots issued since the last drain
+      auto drain = [&]() {
+        comm->wait_async(keys.data(), pending);
+        // (0 = some rank's F does not fit: it stays the minimum and forces the fallback)
+        for (int b = 0; b < pending; ++b) key = std::min(key, keys[b]);
+        pending = 0;
+      };
       if (!cpu && !hybrid) {
         rs = RunStats();
         for (int b = 0; b < npass; ++b) {
@@ -438,15 +479,14 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
             solver->run(i1 - i0, local.off.data() + i0, local.ids.data(), F.data() + i0,
                         a.json ? E2.data() + i0 : nullptr, &rs, stream);
           if (b + 1 == npass) maybe_inject("compute", comm->rank());
-          comm->allreduce_min_u64_async(pack(i0, i1), b);
+          if (pending == nslots) drain();
+          comm->allreduce_min_u64_async(pack(i0, i1), pending++);
         }
       } else {
         maybe_inject("compute", comm->rank());
-        comm->allreduce_min_u64_async(pack(0, nlocal), 0);
+        comm->allreduce_min_u64_async(pack(0, nlocal), pending++);
       }
-      comm->wait_async(keys.data(), npass);
-      uint64_t key = NONE;
-      for (int b = 0; b < npass; ++b) key = std::min(key, keys[b]);
+      drain();
       if (key == NONE) { minF = -1; minK = -1; }
       else if (key != 0) {
         --key;
@@ -543,6 +583,8 @@ int main(int argc, char* argv[]) {
     else if (!strcmp(argv[i], "--threads") && has) a.threads = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--repeat") && has) a.repeat = std::max(1, atoi(argv[++i]));
     else if (!strcmp(argv[i], "--spmd") && has) a.spmd = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--max-words") && has) a.max_words = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--async-slots") && has) a.async_slots = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--cache")) a.cache = true;
     else if (!strcmp(argv[i], "--no-cache")) a.cache = false;
     else if (!strcmp(argv[i], "--json")) a.json = true;
@@ -564,6 +606,11 @@ int main(int argc, char* argv[]) {
         std::vector<int> devs(a.spmd);
         for (int r = 0; r < a.spmd; ++r) devs[r] = (r % a.numGPU) % ndev;
         comms = upgrade_thread_comms_rccl(std::move(comms), devs);
+        // (as maybe_upgrade_rccl: RCCL needs one rank per GPU; never a silent fallback)
+        if (a.comm == "rccl" && comms[0]->name() != "rccl")
+          fprintf(stderr, "msbfs: --comm rccl needs one rank per GPU (--spmd %d over %d device(s)); "
+                  "falling back to the in-process thread collectives\n", a.spmd,
+                  std::min(a.numGPU, ndev));
       }
       std::vector<int> rcs(a.spmd, 0);
       std::vector<std::thread> th;

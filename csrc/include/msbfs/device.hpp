@@ -102,6 +102,10 @@ struct RunStats {
 // ---- device-graph construction (kernels/gen.hip) -------------------------------------------
 void device_graph_from_host(DeviceGraph& g, int64_t n, const int64_t* rowptr, const int32_t* col,
                             hipStream_t s);
+// The legacy graph file (main.cu:92-130) built into a CSR on the device: the mapped edge list is
+// streamed to HBM through pinned staging, then degree count (atomics) -> scan -> scatter, ids
+// validated on the device. Neighbour order is not the file's (F does not depend on it).
+void device_graph_from_edge_file(DeviceGraph& g, const std::string& path, hipStream_t s);
 void device_graph_from_edges(DeviceGraph& g, int64_t n, int64_t m, const int32_t* d_u,
                              const int32_t* d_v, hipStream_t s);
 void device_graph_gen_rmat(DeviceGraph& g, int scale, int64_t edgefactor, uint64_t seed, double a,

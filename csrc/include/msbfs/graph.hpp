@@ -2,6 +2,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -42,6 +43,16 @@ struct EdgeList {
 // graph: int32 n | int64 m | m x {int32 u, int32 v}, little endian, no header magic.
 EdgeList read_edge_list_bin(const std::string& path);
 void write_edge_list_bin(const std::string& path, const EdgeList& el);
+// The legacy graph file mapped read-only and header-checked (size vs m), without copying the
+// edges: the device CSR build (device_graph_from_edge_file) streams them straight to HBM.
+struct EdgeFileMap {
+  int64_t n = 0, m = 0;
+  const uint8_t* edges = nullptr;  // m x {int32 u, int32 v}
+  std::shared_ptr<void> keep;      // the mapping
+};
+EdgeFileMap map_edge_file(const std::string& path);
+// memcpy split over nthreads host threads (page-cache -> pinned staging)
+void parallel_memcpy(void* dst, const void* src, size_t bytes, int nthreads = 0);
 // query: uint8 K | K x {uint8 size | size x int32}. Extended (K or a size > 255): byte 0 is 0
 // (a legacy K=0 file is exactly one byte long), followed by magic "MSBFSQX1", uint32 K and
 // K x {uint32 size | size x int32}. The legacy reader path is bit-exact with main.cu:134-164.

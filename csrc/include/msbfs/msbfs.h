@@ -90,6 +90,9 @@ int msbfs_graph_wrap_device(int device, int64_t n, int64_t nnz, int64_t* d_rowpt
 int msbfs_graph_gen_rmat(int device, int scale, int64_t edgefactor, uint64_t seed, double a,
                          double b, double c, int scramble, msbfs_graph* out);
 int msbfs_graph_gen_uniform(int device, int64_t n, int64_t m, uint64_t seed, msbfs_graph* out);
+/* the legacy edge-list file (main.cu:92-130) built into a CSR on the device (streamed upload,
+ * device count -> scan -> scatter; no host edge arrays) */
+int msbfs_graph_from_edge_file(int device, const char* path, msbfs_graph* out);
 int msbfs_graph_sort_rows(msbfs_graph g);
 /* Renumber vertices by descending degree (hubs first, rows sorted). Queries keep using the
  * original ids: solvers map sources through the stored old->new map. */

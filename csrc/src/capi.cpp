@@ -278,6 +278,16 @@ int msbfs_graph_gen_uniform(int device, int64_t n, int64_t m, uint64_t seed, msb
   });
 }
 
+int msbfs_graph_from_edge_file(int device, const char* path, msbfs_graph* out) {
+  return guard([&] {
+    MSBFS_HIP_CHECK(hipSetDevice(device));
+    auto h = std::make_unique<msbfs_graph_s>();
+    h->g.device = device;
+    msbfs::device_graph_from_edge_file(h->g, path ? path : "", nullptr);
+    *out = h.release();
+  });
+}
+
 int msbfs_graph_sort_rows(msbfs_graph g) {
   return guard([&] {
     MSBFS_HIP_CHECK(hipSetDevice(g->g.device));

@@ -77,6 +77,46 @@ void write_all(FILE* f, const void* p, size_t n, const std::string& path) {
 }
 }  // namespace
 
+EdgeFileMap map_edge_file(const std::string& path) {
+  auto mf = std::make_shared<MappedFile>(path, "graph");
+  if (mf->size < 12) fail("graph file " + path + " is truncated (need 12-byte header)");
+  int32_t n;
+  int64_t m;
+  std::memcpy(&n, mf->bytes(), 4);
+  std::memcpy(&m, mf->bytes() + 4, 8);
+  if (n < 0 || m < 0) fail("graph file " + path + " has a negative n or m");
+  const uint64_t need = 12ull + 8ull * (uint64_t)m;
+  if (mf->size < need)
+    fail("graph file " + path + " is truncated: header says m=" + std::to_string(m) +
+         " edges but the file holds " + std::to_string((mf->size - 12) / 8));
+  EdgeFileMap f;
+  f.n = n;
+  f.m = m;
+  f.edges = mf->bytes() + 12;
+  f.keep = mf;
+  return f;
+}
+
+void parallel_memcpy(void* dst, const void* src, size_t bytes, int nthreads) {
+  if (nthreads <= 0) nthreads = default_threads();
+  constexpr size_t kGrain = size_t(1) << 22;
+  const int64_t pieces = (int64_t)((bytes + kGrain - 1) / kGrain);
+  if (pieces <= 1 || nthreads <= 1) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  std::atomic<int64_t> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < std::min<int64_t>(nthreads, pieces); ++t)
+    th.emplace_back([&] {
+      for (int64_t i; (i = next.fetch_add(1)) < pieces;) {
+        const size_t o = (size_t)i * kGrain;
+        std::memcpy((char*)dst + o, (const char*)src + o, std::min(kGrain, bytes - o));
+      }
+    });
+  for (auto& x : th) x.join();
+}
+
 EdgeList read_edge_list_bin(const std::string& path) {
   MappedFile mf(path, "graph");
   if (mf.size < 12) fail("graph file " + path + " is truncated (need 12-byte header)");

@@ -1,0 +1,309 @@
+// Bit-parallel MS-BFS: the full (unfiltered) pull of the later bottom-up levels — the second
+// pull level on (RMAT-26 / 1024 groups: level 3, 32.5M active vertices, ~140M neighbour rows), the
+// lean pass's overflow list and the device-driven pull batches (bu_batch).
+//
+// Same algorithm as k_bu_narrow without the probe / prefix / snapshot machinery (these levels load
+// every neighbour row): G lanes per vertex, CS neighbours per step, early exit once every alive
+// group is covered. Round-4 changes, from the level-3 ISA and counters of k_bu_narrow (5.6 ms,
+// 3.0 TB/s, ~310 VALU per tile, six block barriers per tile):
+//  * rows move with STRUCTURED buffer loads / stores (index = vertex id, stride = one row, lane
+//    offset = its slot): no 64-bit address arithmetic per row, and a neighbour slot past the end
+//    of the row carries index -1, which the descriptor's range check (index >= n) turns into a
+//    zero row without a branch or a memory request;
+//  * a step's column ids are broadcast inside the lane group with ds_swizzle (constant pattern,
+//    all CS issued before the first use) instead of one ds_bpermute + wait + branch per row;
+//  * the new lists (next active, next wide, new frontier) go through WAVE-private LDS queues with
+//    one global atomic per flush (no __syncthreads in the tile loop: the four waves of a block
+//    no longer wait for the slowest one every tile).
+#pragma once
+
+#include <utility>
+
+#include "common.hpp"
+
+namespace msbfs {
+namespace bp {
+
+typedef uint32_t bu4 __attribute__((ext_vector_type(4)));
+typedef uint32_t bu2 __attribute__((ext_vector_type(2)));
+// LLVM's structured buffer intrinsics (hipcc exposes only the raw builtins): vindex * stride +
+// voffset from the descriptor base; vindex >= num_records reads zeros and drops stores
+__device__ bu4 sbuf_load_b128(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
+                              int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
+__device__ bu2 sbuf_load_b64(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
+                             int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v2i32");
+__device__ void sbuf_store_b128(bu4 v, __amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset,
+                                int soffset, int aux) __asm("llvm.amdgcn.struct.ptr.buffer.store.v4i32");
+__device__ void sbuf_store_b64(bu2 v, __amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset,
+                               int soffset, int aux) __asm("llvm.amdgcn.struct.ptr.buffer.store.v2i32");
+
+// Descriptor of a visited buffer: rows of W words, n rows (index >= n reads as zero). The
+// stride field holds 14 bits: rows up to 16 words (128 B).
+template <int W>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint64_t* base, int64_t n) {
+  static_assert(W * 8 < 16384, "descriptor stride");
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)(W * 8), (int)n, 0x00020000);
+}
+// row slice (VW words) of index u at byte offset voff within the row
+template <int VW>
+__device__ __forceinline__ V<VW> ld_row(__amdgpu_buffer_rsrc_t rs, int32_t u, int voff) {
+  V<VW> r;
+  if constexpr (VW == 2) {
+    const bu4 x = sbuf_load_b128(rs, u, voff, 0, 0);
+    r.w[0] = ((uint64_t)x.y << 32) | x.x;
+    r.w[1] = ((uint64_t)x.w << 32) | x.z;
+  } else {
+    const bu2 x = sbuf_load_b64(rs, u, voff, 0, 0);
+    r.w[0] = ((uint64_t)x.y << 32) | x.x;
+  }
+  return r;
+}
+template <int VW>
+__device__ __forceinline__ void st_row(__amdgpu_buffer_rsrc_t rs, int32_t u, int voff,
+                                       const V<VW>& r) {
+  if constexpr (VW == 2) {
+    bu4 x;
+    x.x = (uint32_t)r.w[0];
+    x.y = (uint32_t)(r.w[0] >> 32);
+    x.z = (uint32_t)r.w[1];
+    x.w = (uint32_t)(r.w[1] >> 32);
+    sbuf_store_b128(x, rs, u, voff, 0, 0);
+  } else {
+    bu2 x;
+    x.x = (uint32_t)r.w[0];
+    x.y = (uint32_t)(r.w[0] >> 32);
+    sbuf_store_b64(x, rs, u, voff, 0, 0);
+  }
+}
+
+// lanes below this one among the set bits of a wave mask (v_mbcnt)
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Value of lane (group base + K) for every lane of a group of G lanes (G <= 8 never crosses the
+// 32-lane halves ds_swizzle's bitmask mode works in): and-mask keeps the group bits, or-mask
+// selects the lane.
+template <int G, int K>
+__device__ __forceinline__ int32_t group_bcast(int32_t x) {
+  static_assert(G >= 1 && G <= 32 && K < G, "group");
+  if constexpr (G == 1) {
+    return x;
+  } else {
+    constexpr int kAnd = 0x1F & ~(G - 1);
+    return __builtin_amdgcn_ds_swizzle(x, kAnd | (K << 5));
+  }
+}
+template <int G, int Q, int N, int... Ks>
+__device__ __forceinline__ void bcast_ids(const int32_t (&u)[Q], int32_t (&uc)[N],
+                                          std::integer_sequence<int, Ks...>) {
+  ((uc[Ks] = group_bcast<G, Ks % G>(u[Ks / G])), ...);
+}
+
+// Wave-private LDS queue: items of this wave only; the count is wave-uniform (kept in an SGPR),
+// a flush takes one global atomic for the whole run and writes it out coalesced.
+__device__ __forceinline__ void wq_push(int32_t* q, uint32_t& n, bool pred, int32_t v) {
+  const uint64_t m = __ballot(pred);
+  if (pred) q[n + mbcnt64(m)] = v;
+  n += (uint32_t)__popcll(m);
+}
+__device__ __forceinline__ void wq_flush(int32_t* q, uint32_t& n, int32_t* out, uint32_t* gcnt) {
+  if (!n) return;
+  uint32_t base = 0;
+  if (lane_id() == 0) base = atomicAdd(gcnt, n);
+  base = __builtin_amdgcn_readfirstlane(base);
+  for (uint32_t i = lane_id(); i < n; i += 64) out[base + i] = q[i];
+  n = 0;
+}
+
+// CS neighbours per step; C1 > 0: a first step of only C1 rows (late levels are mostly covered by
+// the first neighbour, rows sorted hubs first). nact_dev: list length on the device (device-driven
+// levels). gate: closed levels of a device-driven batch are no-ops.
+template <int W, int CS = 8, int C1 = 0>
+__global__ __launch_bounds__(kBlock, 4) void k_bu_full(
+    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, uint64_t* Wb, int64_t n, const uint64_t* alive, const uint64_t* gmask,
+    uint32_t* done, int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* actw2,
+    int next_wide, uint32_t* slabF, const uint32_t* nact_dev, BuGate gate) {
+  if (!bu_gate_open(gate)) return;  // (uniform)
+  if (nact_dev) nact = (int64_t)*nact_dev;
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  constexpr int C = CS;
+  constexpr int Q = C / G > 0 ? C / G : 1;  // ids loaded per lane per step
+  static_assert(G * Q == C, "a step is whole lane groups");
+  static_assert(C1 == 0 || C1 <= C, "short first step");
+  constexpr bool kCombine = G <= 4;
+  // per-wave queues: next narrow active list, new frontier, next wide list
+  // (a flush when another tile's pushes might not fit: every VPW tiles at most)
+  constexpr int QA = VPW >= 64 ? 512 : 448, QF = QA, QW = 2 * VPW > 64 ? 2 * VPW : 64;
+  static_assert(QW >= 2 * VPW, "a wide push always fits after a flush");
+  __shared__ int32_t qmem[kWaves][QA + QF + QW];
+  __shared__ unsigned long long scratch[kWaves];
+  constexpr int CR = 65;  // bank-skewed counter rows (BitCounter::spill_strided)
+  __shared__ uint32_t cnt[CR * W];
+  for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
+  __syncthreads();
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int wv = threadIdx.x >> 6;
+  int32_t* qa = qmem[wv];
+  int32_t* qf = qa + QA;
+  int32_t* qw = qf + QF;
+  uint32_t na = 0, nf = 0, nw = 0;  // (wave-uniform)
+  const __amdgpu_buffer_rsrc_t rR = row_rsrc<W>(R, n), rO = row_rsrc<W>(Wb, n);
+  const int voff = slot * VW * 8;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  unsigned long long eu = 0, ef = 0, ev = 0;
+  BitCounter<VW> bc;
+  bc.zero();
+  int nadd = 0;
+  // software pipeline (as k_bu_narrow): list entry two tiles ahead, own row / offsets one tile
+  // ahead, the first step's column ids one tile ahead (loaded at the end of the previous tile)
+  const int64_t stride = (int64_t)gridDim.x * TILE, lofs = wv * VPW + sub;
+  int64_t tb = (int64_t)blockIdx.x * TILE;
+  int32_t v1 = -1, v2 = -1;
+  if (tb + lofs < nact) v1 = act[tb + lofs];
+  if (tb + stride + lofs < nact) v2 = act[tb + stride + lofs];
+  V<VW> r1 = ld_row<VW>(rR, v1, voff);  // (v1 = -1: zeros)
+  int64_t b1 = 0;
+  uint32_t d1 = 0;
+  if (v1 >= 0) {
+    b1 = rowptr[v1];
+    d1 = (uint32_t)(rowptr[v1 + 1] - b1);
+  }
+  constexpr int F1 = C1 > 0 ? C1 : C;  // neighbours of the first step
+  int32_t u1[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    u1[q] = (q * G + slot < F1 && (uint32_t)(q * G + slot) < d1) ? col[b1 + q * G + slot] : -1;
+  for (; tb < nact; tb += stride) {
+    const int64_t idx = tb + lofs;
+    const bool valid = idx < nact;
+    const int32_t v = valid ? v1 : 0;
+    const V<VW> r = r1;
+    const int64_t beg = b1, end = b1 + d1;
+    const uint32_t deg = d1;
+    int32_t u0[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) u0[q] = u1[q];
+    // prefetch: row / offsets of the next tile, list entry of the one after
+    v1 = idx + stride < nact ? v2 : -1;
+    r1 = ld_row<VW>(rR, v1, voff);
+    if (v1 >= 0) {
+      b1 = rowptr[v1];
+      d1 = (uint32_t)(rowptr[v1 + 1] - b1);
+    } else {
+      b1 = 0;
+      d1 = 0;
+    }
+    if (idx + 2 * stride < nact) v2 = act[idx + 2 * stride];
+    V<VW> unv = vzero<VW>(), acc = vzero<VW>();
+    bool lane_open = false, rnz = false;
+    if (valid) {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        unv.w[j] = ~r.w[j] & am.w[j];
+        lane_open |= unv.w[j] != 0;
+        rnz |= r.w[j] != 0;
+      }
+    }
+    bool g_open = valid && ((__ballot(lane_open) >> (sub * G)) & L::GBITS);
+    if (g_open) {
+      // first step: the preloaded ids (F1 of them)
+      {
+        int32_t uc[F1];
+        bcast_ids<G, Q, F1>(u0, uc, std::make_integer_sequence<int, F1>{});
+        V<VW> x[F1];
+#pragma unroll
+        for (int c = 0; c < F1; ++c) x[c] = ld_row<VW>(rR, uc[c], voff);
+        bool cov = true;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+#pragma unroll
+          for (int c = 0; c < F1; ++c) acc.w[j] |= x[c].w[j];
+          cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
+        }
+        g_open = (__ballot(!cov) >> (sub * G)) & L::GBITS;
+      }
+      for (int64_t e = beg + F1; g_open && e < end; e += C) {
+        int32_t u[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int64_t ee = e + q * G + slot;
+          u[q] = ee < end ? col[ee] : -1;
+        }
+        int32_t uc[C];
+        bcast_ids<G, Q, C>(u, uc, std::make_integer_sequence<int, C>{});
+        V<VW> x[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) x[c] = ld_row<VW>(rR, uc[c], voff);
+        bool cov = true;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+#pragma unroll
+          for (int c = 0; c < C; ++c) acc.w[j] |= x[c].w[j];
+          cov &= (acc.w[j] & unv.w[j]) == unv.w[j];
+        }
+        // the group runs this loop in lock step (same v); it stops when all its lanes are covered
+        g_open = (__ballot(!cov) >> (sub * G)) & L::GBITS;
+      }
+    }
+    V<VW> nwv;
+    bool anynew = false, notfull = false;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      nwv.w[j] = acc.w[j] & unv.w[j];
+      anynew |= nwv.w[j] != 0;
+      notfull |= (unv.w[j] & ~nwv.w[j]) != 0;
+    }
+    {  // also when nothing is open: Wb may hold the previous batch's rows (invalid lanes: index -1)
+      V<VW> nv;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nwv.w[j];
+      st_row<VW>(rO, valid ? v : -1, voff, nv);
+    }
+    bc.add(nwv);  // (zero for invalid lanes)
+    if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+      bc.template spill_strided<CR>(cnt, slot);
+      nadd = 0;
+    }
+    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
+    const bool g_new = (bn >> (sub * G)) & L::GBITS;
+    const bool g_nf = (bf >> (sub * G)) & L::GBITS;
+    const bool leader = valid && slot == 0;
+    wave_set_bits<kCombine>(done, v, leader && !g_nf);
+    const bool keep = leader && g_nf, app = leader && g_new;
+    if (keep) eu += deg;
+    if (app) ef += deg;
+    {
+      const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
+      wave_set_bits<kCombine>(anyvis, v, leader && g_first);
+      if (leader && g_first) ev += deg;
+    }
+    // third stage: the next tile's first-step ids (its offsets arrived during this tile)
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      u1[q] = (q * G + slot < F1 && (uint32_t)(q * G + slot) < d1) ? col[b1 + q * G + slot] : -1;
+    wq_push(qa, na, keep && (int)deg <= next_wide, v);
+    wq_push(qw, nw, keep && (int)deg > next_wide, v);
+    wq_push(qf, nf, app, v);
+    if (na + VPW > QA) wq_flush(qa, na, act2, &ctr->act2.v);
+    if (nw + VPW > QW) wq_flush(qw, nw, actw2, &ctr->actw2.v);
+    if (nf + VPW > QF) wq_flush(qf, nf, fl2, &ctr->fl2.v);
+  }
+  wq_flush(qa, na, act2, &ctr->act2.v);
+  wq_flush(qw, nw, actw2, &ctr->actw2.v);
+  wq_flush(qf, nf, fl2, &ctr->fl2.v);
+  block_sum_add(eu, &ctr->eu2.v, scratch);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
+  bc.template spill_strided<CR>(cnt, slot);
+  __syncthreads();
+  uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+  for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
+}
+
+}  // namespace bp
+}  // namespace msbfs

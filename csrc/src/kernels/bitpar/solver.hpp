@@ -77,6 +77,10 @@ struct Tuning {
   // hold at most bu_max vertices (0 = host-driven pull levels; needs batch > 1)
   int64_t bu_max = 1 << 20;
   int tiles = 1;       // first pull level over static vertex tiles (bitpar/tiles.hpp)
+  // unfiltered pull levels (the second pull level on, lean overflow, device-driven batches) run
+  // k_bu_full (structured-buffer rows, wave-private list queues; bitpar/pull_full.hpp) instead
+  // of k_bu_narrow
+  int full = 1;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->
   // 12: 13.85 -> 13.32 ms)

@@ -5,6 +5,7 @@
 
 #include "bitpar/init.hpp"
 #include "bitpar/pull.hpp"
+#include "bitpar/pull_full.hpp"
 #include "bitpar/solver.hpp"
 
 namespace msbfs {
@@ -259,13 +260,28 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
             ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s));
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gl;
-        k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
-            touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
-            done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
-            next_wide, slabF<W>(rows), nullptr, nullptr, 0, nullptr, &ctr_.as<Ctr>()->touched.v,
-            nullptr, BuGate{});
+        if (tun_.full)
+          k_bu_full<W, 8, 1><<<gn, kBlock, 0, s>>>(
+              touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
+              done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
+              slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{});
+        else
+          k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
+              touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+              done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
+              next_wide, slabF<W>(rows), nullptr, nullptr, 0, nullptr,
+              &ctr_.as<Ctr>()->touched.v, nullptr, BuGate{});
         MSBFS_HIP_CHECK(hipGetLastError());
+        rows += gn;
+      } else if (FUSE && !filt && tun_.full) {
+        auto kf = short1 ? k_bu_full<W, 8, 1> : k_bu_full<W, 8, 0>;
+        kf<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive,
+                                 sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
+                                 fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+                                 anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
+                                 slabF<W>(rows), nullptr, BuGate{});
         rows += gn;
       } else {
         auto kn = FUSE ? (filt ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, true>
@@ -398,6 +414,21 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
   const auto t0 = std::chrono::steady_clock::now();
   trace::Range range_batch("bitpar L%u-%u BU batch", level0 + 1, level0 + K);
   auto kn = k_bu_narrow<W, false, kBlock, 0, true, false, false, 8, 1>;
+  const bool full = tun_.full != 0;
+  auto launch = [&](int grid, const int32_t* list, const uint64_t* R, uint64_t* O,
+                    const uint64_t* alive, int32_t* fl_out, Ctr* out, uint32_t* slab,
+                    const uint32_t* len, const BuGate& gate, int p) {
+    if (full)
+      k_bu_full<W, 8, 1><<<grid, kBlock, 0, s>>>(
+          list, 0, g_.rowptr, g_.col, R, O, g_.n, alive, sm.gmask, done_.as<uint32_t>(),
+          act_[p ^ 1].as<int32_t>(), fl_out, out, anyvis_.as<uint32_t>(),
+          actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate);
+    else
+      kn<<<grid, kBlock, 0, s>>>(list, 0, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+                                 done_.as<uint32_t>(), act_[p ^ 1].as<int32_t>(), fl_out, out,
+                                 anyvis_.as<uint32_t>(), INT32_MAX, actw_[p ^ 1].as<int32_t>(),
+                                 next_wide, slab, nullptr, nullptr, 0, nullptr, len, nullptr, gate);
+  };
   for (int i = 0; i < K; ++i) {
     const BuGate gate{slots + i, opt.beta, alpha, i == 0 ? 1 : 0};
     const int p = i & 1;
@@ -405,17 +436,11 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
     uint64_t* O = vis_[S.cur ^ p ^ 1].as<uint64_t>();
     int32_t* fl_out = fl_[S.fc ^ p ^ 1].as<int32_t>();
     const uint64_t* alive = aslot + 16 * i;
-    kn<<<gn, kBlock, 0, s>>>(act_[p].as<int32_t>(), 0, g_.rowptr, g_.col, R, O, alive, sm.gmask,
-                             done_.as<uint32_t>(), act_[p ^ 1].as<int32_t>(), fl_out, slots + i + 1,
-                             anyvis_.as<uint32_t>(), INT32_MAX, actw_[p ^ 1].as<int32_t>(),
-                             next_wide, slabF<W>(0), nullptr, nullptr, 0, nullptr,
-                             &slots[i].act2.v, nullptr, gate);
+    launch(gn, act_[p].as<int32_t>(), R, O, alive, fl_out, slots + i + 1, slabF<W>(0),
+           &slots[i].act2.v, gate, p);
     if (gw)
-      kn<<<gw, kBlock, 0, s>>>(actw_[p].as<int32_t>(), 0, g_.rowptr, g_.col, R, O, alive,
-                               sm.gmask, done_.as<uint32_t>(), act_[p ^ 1].as<int32_t>(), fl_out,
-                               slots + i + 1, anyvis_.as<uint32_t>(), INT32_MAX,
-                               actw_[p ^ 1].as<int32_t>(), next_wide, slabF<W>(gn), nullptr,
-                               nullptr, 0, nullptr, &slots[i].actw2.v, nullptr, gate);
+      launch(gw, actw_[p].as<int32_t>(), R, O, alive, fl_out, slots + i + 1, slabF<W>(gn),
+             &slots[i].actw2.v, gate, p);
     k_level_reduce<W, false><<<W * rg, kBlock, 0, s>>>(slabF<W>(0), slabE<W>(0), rows, rg, sm.F,
                                                        sm.E, aslot + 16 * (i + 1), level0 + 1 + i,
                                                        gate);

@@ -43,13 +43,14 @@ void Tuning::set(const std::string& key, const std::string& v) {
   } else if (key == "bu_max") bu_max = (int64_t)to_num(key, v);
   else if (key == "tiles") tiles = (int)to_num(key, v);
   else if (key == "tiles_code_deg") tiles_code_deg = to_num(key, v);
+  else if (key == "full") full = (int)to_num(key, v);
   else if (key == "dirs") {
     for (char c : v)
       if (c != 'T' && c != 'B' && c != '.') fail("tuning: dirs takes T, B or . per level");
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dirs)");
   }
 }
 

@@ -375,7 +375,9 @@ class DistSolver final : public Solver {
       } else {
         MSBFS_HIP_CHECK(hipMemsetAsync(dist_.p, 0xFF, (size_t)std::max<int64_t>(n, 1) * 4, s));
       }
-      visited_ = 0;
+      // until this group finishes, an exception (caught by the C API guard, the solver living
+      // on) may leave any vertex marked: force the full refill for the next group
+      visited_ = n;
       MSBFS_HIP_CHECK(hipMemsetAsync(ctr_.p, 0, sizeof(Ctr), s));
       if (ns) {
         MSBFS_HIP_CHECK(hipMemcpyAsync(src_.p, qids + qoff[k], ns * sizeof(int32_t),

@@ -8,6 +8,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "msbfs/device.hpp"
+#include "msbfs/graph.hpp"
 
 namespace msbfs {
 namespace {
@@ -69,6 +70,30 @@ __global__ __launch_bounds__(kBlock) void k_edges_pass(const int32_t* eu, const 
     } else {
       col[atomicAdd(&cnt[u], 1ull)] = v;
       col[atomicAdd(&cnt[v], 1ull)] = u;
+    }
+  }
+}
+
+// Edges of the legacy file format ({int32 u, int32 v} pairs, main.cu:108-112) from a device
+// copy: count (scatter = 0) or scatter both directions (main.cu:113-115). An id outside [0, n)
+// (UB in the reference) records the lowest offending edge index in *bad and is skipped.
+__global__ __launch_bounds__(kBlock) void k_pairs_pass(const int2* e, int64_t m, int64_t e0,
+                                                       int64_t n, unsigned long long* cnt,
+                                                       int32_t* col, int scatter,
+                                                       unsigned long long* bad) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    const int2 uv = e[i];
+    if ((uint32_t)uv.x >= (uint64_t)n || (uint32_t)uv.y >= (uint64_t)n) {
+      atomicMin(bad, (unsigned long long)(e0 + i));
+      continue;
+    }
+    if (!scatter) {
+      atomicAdd(&cnt[uv.x], 1ull);
+      atomicAdd(&cnt[uv.y], 1ull);
+    } else {
+      col[atomicAdd(&cnt[uv.x], 1ull)] = uv.y;
+      col[atomicAdd(&cnt[uv.y], 1ull)] = uv.x;
     }
   }
 }
@@ -246,6 +271,81 @@ void device_graph_from_edges(DeviceGraph& g, int64_t n, int64_t m, const int32_t
                                                        g.col, 1);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
+  device_graph_stats(g, s);
+}
+
+// Host -> device upload of the mapped edge list through two pinned staging buffers: the
+// threads copy piece i + 1 out of the page cache while the DMA engine moves piece i.
+// fn(dev_ptr, first_edge, edges) runs on stream s after each piece landed in `dst` (dst =
+// nullptr: one reused device piece buffer per staging buffer, fn consumes it in place).
+template <class F>
+static void stream_edges(const EdgeFileMap& f, int2* dst, hipStream_t s, F&& fn) {
+  constexpr int64_t kPiece = int64_t(1) << 25;  // edges per piece (256 MB)
+  const int64_t piece = std::min<int64_t>(kPiece, std::max<int64_t>(f.m, 1));
+  PinnedBuf pin0((size_t)piece * 8), pin1((size_t)piece * 8);
+  PinnedBuf* pin[2] = {&pin0, &pin1};
+  DevBuf dpiece[2];
+  if (!dst)
+    for (auto& d : dpiece) d.alloc((size_t)piece * 8);
+  hipEvent_t ev[2];
+  for (auto& e : ev) MSBFS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  bool used[2] = {false, false};
+  int k = 0;
+  for (int64_t e0 = 0; e0 < f.m; e0 += piece, k ^= 1) {
+    const int64_t len = std::min(piece, f.m - e0);
+    if (used[k]) MSBFS_HIP_CHECK(hipEventSynchronize(ev[k]));  // staging k free again
+    parallel_memcpy(pin[k]->p, f.edges + 8 * e0, (size_t)len * 8);
+    int2* d = dst ? dst + e0 : dpiece[k].as<int2>();
+    MSBFS_HIP_CHECK(hipMemcpyAsync(d, pin[k]->p, (size_t)len * 8, hipMemcpyHostToDevice, s));
+    fn(d, e0, len);
+    MSBFS_HIP_CHECK(hipEventRecord(ev[k], s));
+    used[k] = true;
+  }
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  for (auto& e : ev) (void)hipEventDestroy(e);
+}
+
+void device_graph_from_edge_file(DeviceGraph& g, const std::string& path, hipStream_t s) {
+  const EdgeFileMap f = map_edge_file(path);
+  alloc_rowptr(g, f.n);
+  g.m = f.m;
+  const int64_t n = f.n, m = f.m;
+  DevBuf cnt((size_t)std::max<int64_t>(n, 1) * sizeof(int64_t));
+  MSBFS_HIP_CHECK(hipMemsetAsync(cnt.p, 0, cnt.bytes, s));
+  DevBuf bad(sizeof(unsigned long long));
+  MSBFS_HIP_CHECK(hipMemsetAsync(bad.p, 0xFF, bad.bytes, s));
+  // the whole edge list in HBM when it fits next to the CSR (one pass over the file: count and
+  // scatter read the device copy); otherwise the file is streamed twice
+  size_t fr = 0, tot = 0;
+  MSBFS_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+  const size_t ebytes = (size_t)m * 8, cbytes = (size_t)m * 8 + (size_t)n * 24;
+  const bool resident = ebytes + cbytes + (size_t(4) << 30) < fr;
+  DevBuf all;
+  if (resident && m) all.alloc(ebytes);
+  auto pass = [&](int scatter) {
+    auto run = [&](const int2* d, int64_t e0, int64_t len) {
+      k_pairs_pass<<<grid_for(len, kBlock, 8192), kBlock, 0, s>>>(
+          d, len, e0, n, cnt.as<unsigned long long>(), scatter ? g.col : nullptr, scatter,
+          bad.as<unsigned long long>());
+      MSBFS_HIP_CHECK(hipGetLastError());
+    };
+    if (resident && scatter) {
+      if (m) run(all.as<int2>(), 0, m);
+    } else if (m) {
+      // (count pass of the resident mode: upload into `all`, count each piece as it lands)
+      stream_edges(f, resident ? all.as<int2>() : nullptr, s, run);
+    }
+    unsigned long long b = ~0ull;
+    MSBFS_HIP_CHECK(hipMemcpyAsync(&b, bad.p, sizeof(b), hipMemcpyDeviceToHost, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    if (b != ~0ull)
+      fail("graph file " + path + ": edge " + std::to_string(b) +
+           " has a vertex id outside [0, n)");
+  };
+  pass(0);
+  build_from_counts(g, cnt, s);
+  pass(1);
+  g.rows_sorted = false;
   device_graph_stats(g, s);
 }
 

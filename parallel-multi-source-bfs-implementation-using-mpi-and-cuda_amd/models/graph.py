@@ -171,6 +171,16 @@ class DeviceGraph:
         return g.relabel_by_degree() if relabel else g
 
     @classmethod
+    def from_file(cls, path: str, device: int = 0, relabel: bool = False) -> "DeviceGraph":
+        """Build the CSR of a legacy graph file (main.cu:92-130) on the device: the mapped edge
+        list is streamed to HBM and counted / scattered there (no host CSR build)."""
+        h = C.c_void_p()
+        native.check(native.lib().msbfs_graph_from_edge_file(device, str(path).encode(),
+                                                             C.byref(h)))
+        g = cls(h, device)
+        return g.relabel_by_degree() if relabel else g
+
+    @classmethod
     def uniform(cls, n: int, m: int, seed: int = 1, device: int = 0) -> "DeviceGraph":
         h = C.c_void_p()
         native.check(native.lib().msbfs_graph_gen_uniform(device, n, m, seed, C.byref(h)))

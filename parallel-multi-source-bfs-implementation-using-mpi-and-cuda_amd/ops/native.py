@@ -88,6 +88,7 @@ def _sig(lib):
         "msbfs_graph_gen_rmat": (C.c_int, [C.c_int, C.c_int, C.c_int64, C.c_uint64, C.c_double,
                                            C.c_double, C.c_double, C.c_int, P(vp)]),
         "msbfs_graph_gen_uniform": (C.c_int, [C.c_int, C.c_int64, C.c_int64, C.c_uint64, P(vp)]),
+        "msbfs_graph_from_edge_file": (C.c_int, [C.c_int, C.c_char_p, P(vp)]),
         "msbfs_graph_sort_rows": (C.c_int, [vp]),
         "msbfs_graph_relabel_by_degree": (C.c_int, [vp]),
         "msbfs_graph_relabel_map": (C.c_int, [vp, i32p]),

@@ -254,3 +254,78 @@ def gather_F(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistContex
     full = np.zeros(K, dtype=np.int64)
     full[np.asarray(idx_local, dtype=np.int64)] = F_local
     return allreduce_sum_i64(full, ctx)
+
+
+def allgather_int(x: int, ctx: DistContext) -> list:
+    """Every rank's value of x, in rank order (e.g. the GPU ordinal each rank drives)."""
+    if not ctx.distributed:
+        return [int(x)]
+    vec = np.zeros(ctx.world, dtype=np.int64)
+    vec[ctx.rank] = int(x)
+    return [int(v) for v in allreduce_sum_i64(vec, ctx)]
+
+
+def agree_ok(ok: bool, ctx: DistContext) -> bool:
+    """True on every rank iff ok is True on every rank (one MAX all-reduce)."""
+    return allreduce_max(0.0 if ok else 1.0, ctx) == 0.0
+
+
+def checked(fn, ctx: DistContext, what: str = "step"):
+    """Run a rank-local piece of work (no collectives inside) and agree on its success before
+    anyone moves on to the next collective: a failure on one rank raises on EVERY rank instead
+    of leaving the others blocked in a collective the failed rank never joins."""
+    err, out = None, None
+    try:
+        out = fn()
+    except Exception as e:  # noqa: BLE001
+        err = e
+    if not agree_ok(err is None, ctx):
+        if err is not None:
+            raise err
+        raise RuntimeError(f"{what} failed on another rank")
+    return out
+
+
+def evaluate_candidates(candidates, run, reference, ctx: DistContext, reps: int = 1,
+                        required: str = "roundrobin", sync=None):
+    """Time each decomposition candidate (untimed selection pass of bench.py) and drop the ones
+    that fail, collectively: every rank reaches the same decisions, so no rank is ever left
+    alone in a collective the others skipped.
+
+    run(name) -> (F_full, stats) executes one step of candidate `name` and returns the GATHERED
+    F vector (identical on every rank); reference is the F vector it must equal. run must wrap
+    its rank-local work in checked() (between collectives), so that a failure surfaces on every
+    rank at the same point. A candidate
+    that raises on any rank, or whose F differs, is excluded and its reason recorded. Returns
+    (ms, errors): ms[name] = best wall ms over `reps` runs (max over ranks), errors[name] =
+    reason. The `required` candidate (round robin, the reference's own decomposition,
+    main.cu:303-307) failing is reported to the caller, who must not time anything else.
+    """
+    import time
+    ms, errors = {}, {}
+    for name in candidates:
+        for _ in range(max(1, reps)):
+            err, dt, F = "", 0.0, None
+            try:
+                barrier(ctx)
+                if sync:
+                    sync()
+                t = time.perf_counter()
+                F, _ = run(name)
+                if sync:
+                    sync()
+                dt = time.perf_counter() - t
+            except Exception as e:  # noqa: BLE001 (any failure excludes the candidate)
+                err = f"{type(e).__name__}: {e}"[:240]
+            if not agree_ok(not err, ctx):
+                errors[name] = err or "failed on another rank"
+                break
+            t_max = allreduce_max(dt, ctx) * 1e3
+            if not np.array_equal(np.asarray(F), np.asarray(reference)):
+                bad = np.flatnonzero(np.asarray(F) != np.asarray(reference))[:4]
+                errors[name] = f"F differs from the round-robin pass at groups {bad.tolist()}"
+                break
+            ms[name] = min(ms.get(name, t_max), t_max)
+        if name in errors:
+            ms.pop(name, None)
+    return ms, errors

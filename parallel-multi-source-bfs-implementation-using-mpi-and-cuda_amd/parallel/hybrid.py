@@ -212,12 +212,22 @@ class HybridRunner:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t.cpu().numpy()
 
-    def run(self, queries) -> HybridResult:
+    def run(self, queries, checked: bool = False) -> HybridResult:
+        """One hybrid step. checked=True (bench.py's untimed selection pass): every rank-local
+        phase is followed by an agreement all-reduce, so a failure on one rank raises on all of
+        them instead of leaving the others in the exchange (distributed.checked)."""
         if queries.K != self.K:
             raise ValueError("query count differs from the plan")
         ctx, P = self.ctx, self.ctx.world
-        out, sa = self.solver.hybrid_phase_a(queries, ctx.rank, P, self.n_eff, ctx.rank == 0,
-                                             self.wbeg, self.send.data_ptr(), coded=self.coded)
+
+        def local(fn, what):
+            return D.checked(fn, ctx, what) if checked else fn()
+
+        t0 = time.perf_counter()
+        out, sa = local(lambda: self.solver.hybrid_phase_a(
+            queries, ctx.rank, P, self.n_eff, ctx.rank == 0, self.wbeg, self.send.data_ptr(),
+            coded=self.coded), "hybrid phase A")
+        t1 = time.perf_counter()  # (phase A returns host sums: its kernels are done)
         if self.coded:
             # one SUM all-reduce: phase-A partial sums + the P x P matrix of coded lengths
             ext = np.zeros(len(out) + P * P, dtype=np.int64)
@@ -235,13 +245,18 @@ class HybridRunner:
             reduced = self._allreduce(out.copy())
             self._all_to_all(self.recv, self.send, rsz, ssz)
         self.last_bytes = (8 * sum(ssz), 8 * sum(rsz))
-        Fc, sc = self.solver.hybrid_phase_c(self.K, int(self.wbeg[ctx.rank]), self.nw, P,
-                                            self.n_eff, self.recv.data_ptr(), reduced)
+        t2 = time.perf_counter()  # (the exchange synchronises before returning)
+        Fc, sc = local(lambda: self.solver.hybrid_phase_c(
+            self.K, int(self.wbeg[ctx.rank]), self.nw, P, self.n_eff, self.recv.data_ptr(),
+            reduced), "hybrid phase C")
+        t3 = time.perf_counter()
         F = reduced[self.idx] + Fc[:len(self.idx)]
         stats = {"levels": sa.get("levels", 0) + sc.get("levels", 0),
                  "td_levels": sa.get("td_levels", 0) + sc.get("td_levels", 0),
                  "bu_levels": sa.get("bu_levels", 0) + sc.get("bu_levels", 0),
                  "phase_a_ms": sa.get("device_ms"), "phase_c_ms": sc.get("device_ms"),
+                 "phase_a_wall_ms": (t1 - t0) * 1e3, "exchange_ms": (t2 - t1) * 1e3,
+                 "phase_c_wall_ms": (t3 - t2) * 1e3,
                  "part": (ctx.rank, P, self.n_eff), "words": self.nw,
                  "sent_bytes": self.last_bytes[0], "coded": self.coded}
         return HybridResult(self.idx, F, stats)

@@ -90,10 +90,45 @@ def test_bench_multi_rank_gloo_shared_gpu(ranks, dist):
     assert r.returncode == 0, r.stderr[-3000:]
     js = json.loads(r.stdout.strip().splitlines()[-1])
     assert js["n_gpus"] == ranks and js["value"] > 0
+    cfg = js["config"]
+    assert cfg["devices"] == [0] * ranks and cfg["process_group_size"] == ranks
+    assert cfg["candidate_errors"] == {}
     if dist.startswith("hybrid"):
-        assert js["config"]["parallelism"].startswith(f"hybrid{ranks}")
+        assert cfg["parallelism"].startswith(f"hybrid{ranks}")
+        ph = cfg["phases"]  # per-phase wall ms (max over ranks) and the exchange rate
+        assert ph["phase_a_wall_ms"] > 0 and ph["phase_c_wall_ms"] > 0 and ph["exchange_ms"] > 0
+        assert ph["alltoall_GBps_per_rank"] is None or ph["alltoall_GBps_per_rank"] > 0
     else:
-        assert set(js["config"]["candidates_ms"]) == {"roundrobin", "hybrid", "hybrid-coded"}
+        assert set(cfg["candidates_ms"]) == {"roundrobin", "hybrid", "hybrid-coded"}
+
+
+@pytest.mark.parametrize("bad", ["hybrid", "hybrid-coded"])
+def test_bench_excludes_wrong_candidate(bad):
+    """A decomposition whose F is wrong (bench.py --test-corrupt, tests only) is excluded on
+    every rank and reported in candidate_errors; the run still times a verified one (exit 0)."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus",
+                        "2", "--scale", "16", "--groups", "200", "--steps", "2", "--warmup", "1",
+                        "--backend", "gloo", "--verify", "4", "--test-corrupt", bad],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    cfg = js["config"]
+    assert list(cfg["candidate_errors"]) == [bad] and "F differs" in cfg["candidate_errors"][bad]
+    assert bad not in cfg["candidates_ms"] and "roundrobin" in cfg["candidates_ms"]
+    assert js["value"] > 0 and cfg["timed_F_equals_untimed"]
+
+
+def test_bench_wrong_roundrobin_fails():
+    """Round robin itself wrong: no number (exit 3), whatever the other candidates say."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus",
+                        "2", "--scale", "14", "--groups", "100", "--steps", "1", "--warmup", "0",
+                        "--backend", "gloo", "--test-corrupt", "roundrobin"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode != 0
 
 
 def test_bench_gpus_flag_launches_ranks():

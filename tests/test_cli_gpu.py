@@ -172,3 +172,20 @@ def test_cli_gpu_rccl_repeat_multipass(tmp_path, msbfs_pkg):
               "--comm", "rccl", "--repeat", "3", "--json"])
     js = _check(r, ref, m, 1)
     assert js["comm"] == "rccl"
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+@pytest.mark.parametrize("ranks,comm", [(1, "rccl"), (2, "mpi")])
+def test_cli_gpu_many_passes_drain(tmp_path, msbfs_pkg, ranks, comm):
+    """more solver passes than asynchronous reduction slots. --max-words 1 makes every
+    pass 64 groups (700 groups: 11 passes on one rank, 6 on each of two) and --async-slots 2
+    drains the in-flight MIN reductions every 2 passes into the running minimum; the answer must
+    still be the oracle's (before, more passes than slots aborted the job)."""
+    m = msbfs_pkg
+    g, qs, gp, qp = _files(tmp_path, m, 700, 3)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    r = _run([MPIEXEC, "-n", str(ranks), _cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo",
+              "bitpar", "--comm", comm, "--dist", "roundrobin", "--max-words", "1",
+              "--async-slots", "2", "--repeat", "2", "--json"])
+    js = _check(r, ref, m, ranks)
+    assert js["comm"] == comm
