@@ -48,6 +48,29 @@ void Comm::alltoallv_device_u64(const uint64_t* send, const std::vector<int64_t>
   MSBFS_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+void Comm::alltoallv_piece_u64(const uint64_t* send, const std::vector<int64_t>& soff,
+                               const std::vector<int64_t>& scount, uint64_t* recv,
+                               const std::vector<int64_t>& roff,
+                               const std::vector<int64_t>& rcount, hipStream_t s) {
+  int64_t ns = 0, nr = 0;
+  for (int64_t c : scount) ns += c;
+  for (int64_t c : rcount) nr += c;
+  std::vector<uint64_t> hs(std::max<int64_t>(ns, 1)), hr(std::max<int64_t>(nr, 1));
+  int64_t o = 0;
+  for (size_t j = 0; j < scount.size(); o += scount[j], ++j)
+    if (scount[j])
+      MSBFS_HIP_CHECK(hipMemcpyAsync(hs.data() + o, send + soff[j], scount[j] * 8,
+                                     hipMemcpyDeviceToHost, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+  alltoallv_host_u64(hs.data(), scount, hr.data(), rcount);
+  o = 0;
+  for (size_t r = 0; r < rcount.size(); o += rcount[r], ++r)
+    if (rcount[r])
+      MSBFS_HIP_CHECK(hipMemcpyAsync(recv + roff[r], hr.data() + o, rcount[r] * 8,
+                                     hipMemcpyHostToDevice, s));
+  MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+}
+
 void Comm::allreduce_min_u64_async(uint64_t x, int slot) {
   if (slot < 0 || slot >= kAsyncSlots) fail("async all-reduce slot out of range");
   if ((int)async_vals_.size() <= slot) async_vals_.resize(slot + 1, ~0ull);
@@ -294,6 +317,8 @@ class RcclComm final : public Comm {
     if (scratch_) (void)hipFree(scratch_);
     if (hstage_) (void)hipHostFree(hstage_);
     if (hkeys_) (void)hipHostFree(hkeys_);
+    if (piece_ev_) (void)hipEventDestroy(piece_ev_);
+    if (done_ev_) (void)hipEventDestroy(done_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
   int rank() const override { return host_->rank(); }
@@ -355,6 +380,28 @@ class RcclComm final : public Comm {
                           uint64_t* recv, const std::vector<int64_t>& rcount) override {
     host_->alltoallv_host_u64(send, scount, recv, rcount);
   }
+  // a piece of the overlapped exchange: the comm stream waits for the caller's stream (the pack
+  // of this piece), then one grouped send/recv round runs there while the caller goes on
+  void alltoallv_piece_u64(const uint64_t* send, const std::vector<int64_t>& soff,
+                           const std::vector<int64_t>& scount, uint64_t* recv,
+                           const std::vector<int64_t>& roff, const std::vector<int64_t>& rcount,
+                           hipStream_t s) override {
+    MSBFS_HIP_CHECK(hipEventRecord(piece_ev_, s));
+    MSBFS_HIP_CHECK(hipStreamWaitEvent(stream_, piece_ev_, 0));
+    const int P = size();
+    NCCL_CHECK(ncclGroupStart());
+    for (int j = 0; j < P; ++j) {
+      if (scount[j])
+        NCCL_CHECK(ncclSend(send + soff[j], (size_t)scount[j], ncclUint64, j, comm_, stream_));
+      if (rcount[j])
+        NCCL_CHECK(ncclRecv(recv + roff[j], (size_t)rcount[j], ncclUint64, j, comm_, stream_));
+    }
+    NCCL_CHECK(ncclGroupEnd());
+  }
+  void exchange_wait(hipStream_t s) override {
+    MSBFS_HIP_CHECK(hipEventRecord(done_ev_, stream_));
+    MSBFS_HIP_CHECK(hipStreamWaitEvent(s, done_ev_, 0));
+  }
   void alltoallv_device_u64(const uint64_t* send, const std::vector<int64_t>& scount,
                             uint64_t* recv, const std::vector<int64_t>& rcount,
                             hipStream_t s) override {
@@ -383,6 +430,8 @@ class RcclComm final : public Comm {
   uint64_t* key_dev(int slot) const { return (uint64_t*)scratch_ + slot; }
   void setup() {
     MSBFS_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    MSBFS_HIP_CHECK(hipEventCreateWithFlags(&piece_ev_, hipEventDisableTiming));
+    MSBFS_HIP_CHECK(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming));
     MSBFS_HIP_CHECK(hipHostMalloc((void**)&hkeys_, (2 * kAsyncSlots + 2) * 8, hipHostMallocDefault));
     ensure(64 << 10);
   }
@@ -404,6 +453,7 @@ class RcclComm final : public Comm {
   uint64_t* hkeys_ = nullptr;     // pinned: async inputs, async results, one sync slot pair
   size_t cap_ = 0;
   int nasync_ = 0;
+  hipEvent_t piece_ev_ = nullptr, done_ev_ = nullptr;  // overlapped exchange ordering
 };
 #endif
 

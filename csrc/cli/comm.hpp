@@ -51,6 +51,17 @@ class Comm {
                                     hipStream_t s);
   virtual void alltoallv_host_u64(const uint64_t* send, const std::vector<int64_t>& scount,
                                   uint64_t* recv, const std::vector<int64_t>& rcount) = 0;
+  // One piece of a chunked all-to-all between device buffers (the overlapped hybrid exchange):
+  // scount[j] words from send + soff[j] go to rank j, rcount[r] words from rank r land at
+  // recv + roff[r]. Ordered after the work queued on `s` so far; may return before the words
+  // moved (RcclComm: grouped ncclSend/ncclRecv on the communicator's stream while `s` goes on).
+  // exchange_wait(s) orders `s` after every piece issued so far. Default: synchronous, staged
+  // through host memory.
+  virtual void alltoallv_piece_u64(const uint64_t* send, const std::vector<int64_t>& soff,
+                                   const std::vector<int64_t>& scount, uint64_t* recv,
+                                   const std::vector<int64_t>& roff,
+                                   const std::vector<int64_t>& rcount, hipStream_t s);
+  virtual void exchange_wait(hipStream_t s) { (void)s; }
   [[noreturn]] virtual void abort(int code) = 0;
   virtual bool device_collectives() const { return false; }
   // Size persistent device scratch for allreduce_sum_i64 of `bytes` (called before a timed

@@ -48,6 +48,7 @@ struct Args {
   int spmd = 0;
   int max_words = 0;    // bit-parallel: at most 64*max_words groups per solver pass (0: all fit)
   int async_slots = 0;  // asynchronous MIN slots before a drain (0: Comm::kAsyncSlots; tests)
+  int chunks = 0;       // hybrid: pieces of the overlapped exchange (0: 4 with RCCL, else 1)
   bool cache = false, json = false, sort_rows = false, relabel = true;
 };
 
@@ -373,6 +374,22 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
       hout.resize(2 * K + 3 + (hcoded ? (size_t)P * P : 0));
       hF.resize((size_t)std::max(1, 64 * nw_me));
     }
+    // Overlapped exchange (dense): phase A hands out its own-vertex ranges as they are done and
+    // each range's piece of the all-to-all runs while the next one computes (RcclComm: on the
+    // communicator's stream). Every rank's range bounds are agreed on here (one SUM all-reduce).
+    const int nchunks = (hybrid && !hcoded)
+                            ? std::max(1, std::min(a.chunks > 0 ? a.chunks
+                                                                : (comm->device_collectives() ? 4 : 1),
+                                                   256))
+                            : 1;
+    std::vector<int64_t> cbounds;  // [P][nchunks + 1]
+    if (nchunks > 1) {
+      cbounds.assign((size_t)P * (nchunks + 1), 0);
+      solver->hybrid_chunk_bounds(me, P, n_eff, nchunks, cbounds.data() + (size_t)me * (nchunks + 1),
+                                  stream);
+      MSBFS_HIP_CHECK(hipStreamSynchronize(stream));
+      comm->allreduce_sum_i64(cbounds.data(), cbounds.size());
+    }
 
     const auto t_pre1 = clk::now();  // main.cu:297-298
     trace::pop();
@@ -429,12 +446,51 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
       } else if (hybrid) {
         // levels 1-2 vertex-partitioned (all groups), one word all-to-all, the rest per rank
         rs = RunStats();
-        solver->hybrid_phase_a(K, q.off.data(), q.ids.data(), me, P, n_eff, me == 0, wbeg.data(),
-                               hsend.as<uint64_t>(), hout.data(), &rs, stream,
-                               hcoded ? clen.data() : nullptr);
+        if (nchunks > 1) {
+          // piece c: own range [b(me, c), b(me, c + 1)) of every destination's word block of
+          // hsend (destination-major), from every rank r its range c straight into r's block of
+          // hrecv (source-major, the layout phase C reads)
+          struct PieceCtx {
+            Comm* comm;
+            const std::vector<int64_t>* b;
+            int P, me, nch, nw_me;
+            const int32_t* wbeg;
+            const std::vector<int64_t>* pcount;
+            uint64_t *send, *recv;
+            hipStream_t s;
+          } pc{comm.get(), &cbounds, P, me, nchunks, nw_me, wbeg.data(), &pcount,
+               hsend.as<uint64_t>(), hrecv.as<uint64_t>(), stream};
+          auto piece = [](void* user, int c, int64_t i0, int64_t i1) {
+            const PieceCtx& x = *(const PieceCtx*)user;
+            std::vector<int64_t> soff(x.P), scnt(x.P), roff(x.P), rcnt(x.P);
+            const int64_t cnt = (*x.pcount)[x.me];
+            int64_t rb = 0;
+            for (int j = 0; j < x.P; ++j) {
+              const int64_t nwj = x.wbeg[j + 1] - x.wbeg[j];
+              soff[j] = cnt * x.wbeg[j] + i0 * nwj;
+              scnt[j] = (i1 - i0) * nwj;
+              const int64_t a0 = (*x.b)[(size_t)j * (x.nch + 1) + c];
+              const int64_t a1 = (*x.b)[(size_t)j * (x.nch + 1) + c + 1];
+              roff[j] = rb + a0 * x.nw_me;
+              rcnt[j] = (a1 - a0) * x.nw_me;
+              rb += (*x.pcount)[j] * x.nw_me;
+            }
+            x.comm->alltoallv_piece_u64(x.send, soff, scnt, x.recv, roff, rcnt, x.s);
+          };
+          solver->hybrid_phase_a(K, q.off.data(), q.ids.data(), me, P, n_eff, me == 0,
+                                 wbeg.data(), hsend.as<uint64_t>(), hout.data(), &rs, stream,
+                                 nullptr, nchunks, piece, &pc);
+        } else {
+          solver->hybrid_phase_a(K, q.off.data(), q.ids.data(), me, P, n_eff, me == 0,
+                                 wbeg.data(), hsend.as<uint64_t>(), hout.data(), &rs, stream,
+                                 hcoded ? clen.data() : nullptr);
+        }
         {
           trace::Range range_x("hybrid exchange");
-          if (hcoded) {
+          if (nchunks > 1) {
+            comm->allreduce_sum_i64(hout.data(), hout.size());
+            comm->exchange_wait(stream);  // (phase C's kernels follow on `stream`)
+          } else if (hcoded) {
             int64_t* M = hout.data() + 2 * K + 3;
             std::fill(M, M + (size_t)P * P, 0);
             for (int j = 0; j < P; ++j) M[(size_t)me * P + j] = clen[j];
@@ -585,6 +641,7 @@ int main(int argc, char* argv[]) {
     else if (!strcmp(argv[i], "--spmd") && has) a.spmd = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--max-words") && has) a.max_words = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--async-slots") && has) a.async_slots = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--chunks") && has) a.chunks = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--cache")) a.cache = true;
     else if (!strcmp(argv[i], "--no-cache")) a.cache = false;
     else if (!strcmp(argv[i], "--json")) a.json = true;

@@ -167,13 +167,31 @@ class Solver {
   // coded_len_host != nullptr: send_dev gets the zero-word coded segments instead (see
   // hybrid_coded_bound / kernels/bitpar.hip "zero-word coding"), coded_len_host[j] = words of
   // destination j's segment; the segments lie back to back in destination order.
+  //
+  // Overlapped (chunked) exchange, dense mode only: `chunks` > 1 splits the own vertices into
+  // index ranges [bounds[c], bounds[c+1]) (hybrid_chunk_bounds: the same split on every call
+  // for one part / nparts / n_eff / chunks). Phase A packs each range into its place in
+  // send_dev as soon as the level-2 pull finished it and calls cb(user, c, bounds[c],
+  // bounds[c+1]) with that pack enqueued on `stream`; the callback starts its piece of the
+  // all-to-all ordered after that point (on the collective's own stream) while the next range
+  // computes. cb runs exactly `chunks` times, in order; send_dev's layout is unchanged.
+  using ChunkFn = void (*)(void* user, int chunk, int64_t i0, int64_t i1);
   virtual void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part,
                               int nparts, int64_t n_eff, bool count_l1, const int32_t* wbeg,
                               uint64_t* send_dev, int64_t* out_host, RunStats* st,
-                              hipStream_t stream, int64_t* coded_len_host = nullptr) {
+                              hipStream_t stream, int64_t* coded_len_host = nullptr,
+                              int chunks = 1, ChunkFn cb = nullptr, void* user = nullptr) {
     (void)K, (void)qoff, (void)qids, (void)part, (void)nparts, (void)n_eff, (void)count_l1,
-        (void)wbeg, (void)send_dev, (void)out_host, (void)st, (void)stream, (void)coded_len_host;
+        (void)wbeg, (void)send_dev, (void)out_host, (void)st, (void)stream, (void)coded_len_host,
+        (void)chunks, (void)cb, (void)user;
     fail("this solver has no hybrid mode (use the bit-parallel solver)");
+  }
+  // bounds[0..chunks]: the own-vertex index ranges of a chunked phase A (see above)
+  virtual void hybrid_chunk_bounds(int part, int nparts, int64_t n_eff, int chunks,
+                                   int64_t* bounds, hipStream_t stream) {
+    (void)stream;
+    const int64_t cnt = n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
+    for (int c = 0; c <= chunks; ++c) bounds[c] = cnt * c / chunks;
   }
   // Receiver side of the coded exchange: coded_dev holds one coded segment per source part r
   // (coded_len_host[r] words each, back to back); dense_dev gets the layout hybrid_phase_c reads.

@@ -152,6 +152,20 @@ int msbfs_solver_hybrid_phase_a_coded(msbfs_solver s, int64_t K, const int64_t* 
                                       int count_l1, const int32_t* wbeg, void* send_dev,
                                       int64_t* out, int64_t* coded_len, msbfs_stats* st,
                                       void* stream);
+/* Overlapped exchange (dense layout): phase A in `chunks` own-vertex ranges
+ * [bounds[c], bounds[c+1]) (msbfs_solver_hybrid_chunk_bounds, bounds[chunks+1]); after each
+ * range's words are packed into send_dev (pack enqueued on `stream`), cb(user, c, i0, i1) runs
+ * on the calling thread: it starts that piece of the all-to-all ordered after `stream` (e.g. an
+ * asynchronous collective on the communicator's stream) while the next range computes. */
+typedef void (*msbfs_chunk_fn)(void* user, int chunk, int64_t i0, int64_t i1);
+int msbfs_solver_hybrid_chunk_bounds(msbfs_solver s, int part, int nparts, int64_t n_eff,
+                                     int chunks, int64_t* bounds);
+int msbfs_solver_hybrid_phase_a_chunked(msbfs_solver s, int64_t K, const int64_t* qoff,
+                                        const int32_t* qids, int part, int nparts,
+                                        int64_t n_eff, int count_l1, const int32_t* wbeg,
+                                        void* send_dev, int64_t* out, int chunks,
+                                        msbfs_chunk_fn cb, void* user, msbfs_stats* st,
+                                        void* stream);
 int msbfs_solver_hybrid_decode(msbfs_solver s, const void* coded_dev, const int64_t* coded_len,
                                int nparts, int64_t n_eff, int w_count, void* dense_dev,
                                void* stream);

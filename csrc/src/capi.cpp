@@ -452,6 +452,32 @@ int msbfs_solver_hybrid_phase_a_coded(msbfs_solver s, int64_t K, const int64_t* 
   });
 }
 
+int msbfs_solver_hybrid_chunk_bounds(msbfs_solver s, int part, int nparts, int64_t n_eff,
+                                     int chunks, int64_t* bounds) {
+  return guard([&] {
+    if (!s || !s->impl) msbfs::fail("null solver");
+    if (chunks < 1 || chunks > 1024) msbfs::fail("hybrid: chunks must be in [1, 1024]");
+    MSBFS_HIP_CHECK(hipSetDevice(s->graph->g.device));
+    s->impl->hybrid_chunk_bounds(part, nparts, n_eff, chunks, bounds, nullptr);
+    MSBFS_HIP_CHECK(hipDeviceSynchronize());
+  });
+}
+
+int msbfs_solver_hybrid_phase_a_chunked(msbfs_solver s, int64_t K, const int64_t* qoff,
+                                        const int32_t* qids, int part, int nparts,
+                                        int64_t n_eff, int count_l1, const int32_t* wbeg,
+                                        void* send_dev, int64_t* out, int chunks,
+                                        msbfs_chunk_fn cb, void* user, msbfs_stats* st,
+                                        void* stream) {
+  return guard([&] {
+    if (!cb) msbfs::fail("hybrid_phase_a_chunked: no chunk callback");
+    timed(s, stream, st, "hybrid phase A", [&](msbfs::RunStats* rs, hipStream_t hs) {
+      s->impl->hybrid_phase_a(K, qoff, qids, part, nparts, n_eff, count_l1 != 0, wbeg,
+                              (uint64_t*)send_dev, out, rs, hs, nullptr, chunks, cb, user);
+    });
+  });
+}
+
 int msbfs_solver_hybrid_decode(msbfs_solver s, const void* coded_dev, const int64_t* coded_len,
                                int nparts, int64_t n_eff, int w_count, void* dense_dev,
                                void* stream) {

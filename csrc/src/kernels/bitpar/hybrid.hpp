@@ -63,10 +63,12 @@ __device__ __forceinline__ int code_seg(const CodeSegs& cs, int nseg, int64_t c)
 // row load per lane; a destination's words of consecutive vertices are contiguous, so the lanes
 // of one slot store adjacent runs (one word per thread with a 64-bit divide and a degree test per
 // word took 0.32 ms per rank at 8 ranks on RMAT-26)
+// (only own-vertex indices i in [i0, i1): a chunked phase A packs each range when it is final)
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, const int64_t* rowptr,
                                                        int part, int nparts, int64_t cnt, int wt,
-                                                       WordSplit ws, uint64_t* send) {
+                                                       WordSplit ws, uint64_t* send, int64_t i0,
+                                                       int64_t i1) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
@@ -82,9 +84,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_words(const uint64_t* vis, cons
     dnw[k] = ws.b[j + 1] - ws.b[j];
     doff[k] = w - ws.b[j];
   }
-  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < cnt; tb += (int64_t)gridDim.x * TILE) {
+  for (int64_t tb = i0 + (int64_t)blockIdx.x * TILE; tb < i1; tb += (int64_t)gridDim.x * TILE) {
     const int64_t i = tb + wv * VPW + sub;
-    if (i >= cnt) continue;
+    if (i >= i1) continue;
     const int64_t v = part + i * nparts;
     const bool deg0 = rowptr[v + 1] == rowptr[v];
     const V<VW> r = deg0 ? vzero<VW>() : ldv<VW>(vis + v * W + slot * VW);

@@ -38,6 +38,7 @@
 #pragma once
 
 #include <chrono>
+#include <functional>
 #include <vector>
 #include <memory>
 #include <string>
@@ -107,8 +108,10 @@ class BitparSolver final : public Solver {
   int64_t hybrid_max_groups() const override { return 64 * (int64_t)maxW_; }
   void hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,
                       int64_t n_eff, bool count_l1, const int32_t* wbeg, uint64_t* send,
-                      int64_t* out, RunStats* st, hipStream_t s,
-                      int64_t* coded_len = nullptr) override;
+                      int64_t* out, RunStats* st, hipStream_t s, int64_t* coded_len = nullptr,
+                      int chunks = 1, ChunkFn cb = nullptr, void* user = nullptr) override;
+  void hybrid_chunk_bounds(int part, int nparts, int64_t n_eff, int chunks, int64_t* bounds,
+                           hipStream_t s) override;
   void hybrid_phase_c(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
                       const uint64_t* recv, const int64_t* reduced, int64_t* F_out, RunStats* st,
                       hipStream_t s) override;
@@ -140,6 +143,12 @@ class BitparSolver final : public Solver {
     bool lean_ran = false;              // this level ran one (its overflow count is c.touched)
     bool old_stale = false;             // k_td_fused levels updated only vis_[cur]
     bool fl_bitmap = false;             // fl_[fc] not built yet: the frontier is in fbm_tile_
+    // chunked hybrid phase A: the tiled level-2 pull runs the own-vertex ranges
+    // [chunk_b[c], chunk_b[c+1]) one after another and calls on_chunk(c) after each (its rows
+    // are final then); chunks_done counts the calls (phase A makes up the rest after the level)
+    std::vector<int64_t> chunk_b;
+    std::function<void(int)> on_chunk;
+    int chunks_done = 0;
   };
   struct Small {
     unsigned long long* F;
@@ -193,6 +202,8 @@ class BitparSolver final : public Solver {
   struct TileSet {
     DevBuf pent, tiles, big;
     int64_t ntiles = 0, nbig = 0, nent = 0;
+    std::vector<int64_t> ti, te;  // host: own-vertex index and first entry of every tile (+ end)
+    int64_t last_partial = -1;    // last tile of a big vertex (they all precede chunk 1)
     int part = -1, nparts = 0;
     const void* key[2] = {nullptr, nullptr};
   };
@@ -210,7 +221,8 @@ class BitparSolver final : public Solver {
   template <int W>
   void phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int part, int nparts,
                     int64_t n_eff, bool count_l1, const int32_t* wbeg, uint64_t* send,
-                    int64_t* out, RunStats* st, hipStream_t s, int64_t* coded_len);
+                    int64_t* out, RunStats* st, hipStream_t s, int64_t* coded_len, int chunks,
+                    ChunkFn cb, void* user);
   template <int W>
   void phase_c_impl(int64_t K, int w_begin, int w_count, int nparts, int64_t n_eff,
                     const uint64_t* recv, const int64_t* reduced, int64_t* F_out, RunStats* st,

@@ -23,7 +23,7 @@ WordSplit word_split(const int32_t* wbeg, int nparts, int wt) {
 void BitparSolver::hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t* qids, int part,
                                   int nparts, int64_t n_eff, bool count_l1, const int32_t* wbeg,
                                   uint64_t* send, int64_t* out, RunStats* st, hipStream_t s,
-                                  int64_t* coded_len) {
+                                  int64_t* coded_len, int chunks, ChunkFn cb, void* user) {
   if (K < 1 || K > hybrid_max_groups())
     fail("hybrid mode: K=" + std::to_string(K) + " groups exceeds one round (" +
          std::to_string(hybrid_max_groups()) + ")");
@@ -34,12 +34,14 @@ void BitparSolver::hybrid_phase_a(int64_t K, const int64_t* qoff, const int32_t*
   if (wbeg[0] != 0 || wbeg[nparts] != wt) fail("hybrid mode: word split must cover ceil(K/64)");
   for (int j = 0; j < nparts; ++j)
     if (wbeg[j + 1] < wbeg[j]) fail("hybrid mode: word split not monotone");
+  if (chunks < 1 || (chunks > 1 && (coded_len || !cb)))
+    fail("hybrid mode: a chunked exchange needs chunks >= 1, the dense layout and a callback");
   int w = 1;
   while (w < wt) w <<= 1;
 #define MSBFS_BP_CASE(WW)                                                                  \
   case WW:                                                                                 \
       phase_a_impl<WW>(K, qoff, qids, part, nparts, n_eff, count_l1, wbeg, send, out, st, s, \
-                     coded_len);                                                             \
+                       coded_len, chunks, cb, user);                                         \
     break;
   switch (w) {
     MSBFS_BP_FOR_W(MSBFS_BP_CASE)
@@ -99,7 +101,7 @@ void BitparSolver::code_send(const uint64_t* vis, uint64_t* staging, int64_t cnt
   if (c == 0) return;
   const CodeWs w = code_ws(c);
   k_pack_words<W><<<grid_for(cnt, Lay<W>::TILE, 8192), kBlock, 0, s>>>(
-      vis, g_.rowptr, part, nparts, cnt, ws.b[nparts], ws, staging);
+      vis, g_.rowptr, part, nparts, cnt, ws.b[nparts], ws, staging, 0, cnt);
   MSBFS_HIP_CHECK(hipGetLastError());
   const int gc = grid_for((c + kCodeCPW - 1) / kCodeCPW * 64, kBlock, 1 << 20);
   k_code_bits<<<gc, kBlock, 0, s>>>(staging, cs, nparts, w.bits, w.pop);
@@ -151,7 +153,7 @@ template <int W>
 void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* qids, int part,
                                 int nparts, int64_t n_eff, bool count_l1, const int32_t* wbeg,
                                 uint64_t* send, int64_t* out, RunStats* st, hipStream_t s,
-                                int64_t* coded_len) {
+                                int64_t* coded_len, int chunks, ChunkFn cb, void* user) {
   Loop S;
   S.part = part;
   S.nparts = nparts;
@@ -160,6 +162,24 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
   S.weight_l1 = count_l1;
   S.plan = "TB";
   S.lazy = tun_.lazy && opt.force_dir == 0 && tun_.dirs.empty();
+  const int wt = (int)((K + 63) / 64);
+  const WordSplit ws = word_split(wbeg, nparts, wt);
+  // pack own-vertex range [i0, i1) of buffer vis into its place in send
+  auto pack = [&](const uint64_t* vis, int64_t i0, int64_t i1) {
+    if (i1 <= i0) return;
+    k_pack_words<W><<<grid_for(i1 - i0, Lay<W>::TILE, 8192), kBlock, 0, s>>>(
+        vis, g_.rowptr, part, nparts, S.cnt, wt, ws, send, i0, i1);
+    MSBFS_HIP_CHECK(hipGetLastError());
+  };
+  if (chunks > 1) {
+    S.chunk_b.resize((size_t)chunks + 1);
+    hybrid_chunk_bounds(part, nparts, n_eff, chunks, S.chunk_b.data(), s);
+    // (called by the tiled level-2 pull after each range: its output buffer is vis_[cur ^ 1])
+    S.on_chunk = [&](int c) {
+      pack(vis_[S.cur ^ 1].as<uint64_t>(), S.chunk_b[(size_t)c], S.chunk_b[(size_t)c + 1]);
+      cb(user, c, S.chunk_b[(size_t)c], S.chunk_b[(size_t)c + 1]);
+    };
+  }
   start_batch<W, false>(0, K, qoff, qids, S, s);
   levels<W, false>(S, st, s);
   if (S.fsrc_acc && S.nf > 0) {  // stopped after a top-down level: restore the zero accumulator
@@ -167,17 +187,19 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
         fl_[S.fc].as<int32_t>(), S.nf, acc_[S.ac].as<uint64_t>());
     MSBFS_HIP_CHECK(hipGetLastError());
   }
-  const int wt = (int)((K + 63) / 64);
-  const WordSplit ws = word_split(wbeg, nparts, wt);
-  if (coded_len) {
+  if (chunks > 1) {
+    // ranges the level did not hand out (no tiled level-2 pull): packed now, in order
+    for (int c = S.chunks_done; c < chunks; ++c) {
+      pack(vis_[S.cur].as<uint64_t>(), S.chunk_b[(size_t)c], S.chunk_b[(size_t)c + 1]);
+      cb(user, c, S.chunk_b[(size_t)c], S.chunk_b[(size_t)c + 1]);
+    }
+  } else if (coded_len) {
     // the dense segments are staged in the other visited buffer (n*maxW words >= cnt*wt; no
     // phase needs its rows any more: phase C and the next batch rewrite or guard every row)
     code_send<W>(vis_[S.cur].as<uint64_t>(), vis_[S.cur ^ 1].as<uint64_t>(), S.cnt, part,
                  nparts, wbeg, send, coded_len, s);
-  } else if (S.cnt > 0) {
-    k_pack_words<W><<<grid_for(S.cnt, Lay<W>::TILE, 8192), kBlock, 0, s>>>(
-        vis_[S.cur].as<uint64_t>(), g_.rowptr, part, nparts, S.cnt, wt, ws, send);
-    MSBFS_HIP_CHECK(hipGetLastError());
+  } else {
+    pack(vis_[S.cur].as<uint64_t>(), 0, S.cnt);
   }
   const bool ran_l2 = S.level >= 2;
   const Small sm = small();

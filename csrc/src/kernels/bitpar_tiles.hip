@@ -115,6 +115,15 @@ const BitparSolver::TileSet* BitparSolver::pfx_tiles(int W, int part, int nparts
   T.ntiles = (int64_t)tl.size() - 1;
   T.nbig = (int64_t)big.size();
   T.nent = nent;
+  T.ti.resize((size_t)T.ntiles + 1);
+  T.te.resize((size_t)T.ntiles + 1);
+  for (int64_t t = 0; t < T.ntiles; ++t) {
+    T.ti[(size_t)t] = ((int64_t)tl[(size_t)t].v0 - part) / nparts;
+    T.te[(size_t)t] = tl[(size_t)t].e0;
+    if (tl[(size_t)t].nv & kTilePartial) T.last_partial = t;
+  }
+  T.ti[(size_t)T.ntiles] = cnt;
+  T.te[(size_t)T.ntiles] = nent;
   if (T.ntiles > 0) {
     k_fill_pent<<<grid_for(T.ntiles * 64, 256, 16384), 256, 0, s>>>(
         T.tiles.as<PfxTile>(), T.ntiles, nparts, g_.rowptr, g_.col, plen, T.pent.as<uint32_t>());
@@ -146,6 +155,32 @@ void BitparSolver::prepare_hybrid(int part, int nparts, hipStream_t s) {
   MSBFS_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+// Own-vertex ranges of a chunked phase A (device.hpp): from the tile set, split at tile starts
+// into pieces of about equal prefix entries; the first piece holds every big vertex's partial
+// tiles (k_bu_wide_finalize runs after it). Without tiles: an even split (the ranges are then
+// packed after the level).
+void BitparSolver::hybrid_chunk_bounds(int part, int nparts, int64_t n_eff, int chunks,
+                                       int64_t* b, hipStream_t s) {
+  if (chunks < 1) fail("hybrid: chunks must be >= 1");
+  const int64_t cnt = n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
+  const TileSet* T = (g_.rows_sorted && g_.n <= INT32_MAX && tun_.pfx == 2 && maxW_ >= 8)
+                         ? pfx_tiles(maxW_, part, nparts, s) : nullptr;
+  if (!T || T->ti.empty() || T->ti.back() != cnt) {
+    for (int c = 0; c <= chunks; ++c) b[c] = cnt * c / chunks;
+    return;
+  }
+  b[0] = 0;
+  int64_t t = 0;
+  for (int c = 1; c < chunks; ++c) {
+    const int64_t target = T->nent * c / chunks;
+    int64_t tc = std::lower_bound(T->te.begin(), T->te.end() - 1, target) - T->te.begin();
+    if (c == 1) tc = std::max(tc, T->last_partial + 1);
+    t = std::max(t, std::min(tc, T->ntiles));
+    b[c] = T->ti[(size_t)t];
+  }
+  b[chunks] = cnt;
+}
+
 // The first pull level of a batch over the tiles (see level_bu: called after the tail push).
 // Returns the slab rows it wrote; leaves the next active lists in act_[1] / actw_[1] and the
 // frontier in fbm_tile_ (S.fl_bitmap).
@@ -163,14 +198,12 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
   MSBFS_HIP_CHECK(hipMemsetAsync(fbm_tile_.p, 0, (size_t)nwords * sizeof(uint32_t), s));
   const uint32_t* pvis = snap ? snap : anyvis_.as<uint32_t>();
   const int grid = std::max(1, num_cus_);
-  k_pfx_tiles<W><<<grid, kTileBlock, 0, s>>>(
-      T->tiles.as<PfxTile>(), T->ntiles, T->pent.as<uint32_t>(), S.nparts, g_.rowptr, R, O,
-      acc_[S.ac].as<uint64_t>(), pvis, snap, codes, codes ? code_from : INT32_MAX, alive,
-      sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), fbm_tile_.as<uint32_t>(),
-      ctr_.as<Ctr>(), slabF<W>(rows), zrow_.as<uint64_t>());
-  MSBFS_HIP_CHECK(hipGetLastError());
-  rows += grid;
-  if (T->nbig) {
+  // tile ranges: one launch for the whole level, or one per own-vertex range of a chunked
+  // hybrid phase A (each range's rows are final once its launch and, for the first, the big
+  // vertices' finalize ran; on_chunk then packs and sends them while the next range computes)
+  const int nch = S.on_chunk && S.chunk_b.size() >= 2 ? (int)S.chunk_b.size() - 1 : 1;
+  auto finalize_big = [&] {
+    if (!T->nbig) return;
     const int gw = grid_for(T->nbig, Lay<W>::TILE, kMaxGrid);
     k_bu_wide_finalize<W, false, true><<<gw, kBlock, 0, s>>>(
         T->big.as<int32_t>(), T->nbig, g_.rowptr, R, O, acc_[S.ac].as<uint64_t>(), alive,
@@ -178,6 +211,28 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
         anyvis_.as<uint32_t>(), nullptr, 0, slabF<W>(rows), snap, fbm_tile_.as<uint32_t>());
     MSBFS_HIP_CHECK(hipGetLastError());
     rows += gw;
+  };
+  int64_t t0 = 0;
+  for (int c = 0; c < nch; ++c) {
+    int64_t t1 = T->ntiles;
+    if (nch > 1 && c + 1 < nch)  // first tile of the next range
+      t1 = std::lower_bound(T->ti.begin(), T->ti.end() - 1, S.chunk_b[(size_t)c + 1]) -
+           T->ti.begin();
+    if (t1 > t0) {
+      k_pfx_tiles<W><<<grid, kTileBlock, 0, s>>>(
+          T->tiles.as<PfxTile>() + t0, t1 - t0, T->pent.as<uint32_t>(), S.nparts, g_.rowptr, R,
+          O, acc_[S.ac].as<uint64_t>(), pvis, snap, codes, codes ? code_from : INT32_MAX, alive,
+          sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), fbm_tile_.as<uint32_t>(),
+          ctr_.as<Ctr>(), slabF<W>(rows), zrow_.as<uint64_t>());
+      MSBFS_HIP_CHECK(hipGetLastError());
+      rows += grid;
+    }
+    if (c == 0) finalize_big();
+    if (nch > 1) {
+      S.on_chunk(c);
+      ++S.chunks_done;
+    }
+    t0 = t1;
   }
   // next active lists (a hybrid phase A stops here: nothing reads them)
   if (S.level < S.stop_level) {

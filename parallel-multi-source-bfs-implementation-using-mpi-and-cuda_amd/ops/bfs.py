@@ -124,6 +124,44 @@ class Solver:
         native.check(native.lib().msbfs_solver_hybrid_phase_a(*args, C.byref(st), strm))
         return out, st.as_dict()
 
+    def hybrid_chunk_bounds(self, part: int, nparts: int, n_eff: int, chunks: int) -> np.ndarray:
+        """Own-vertex index ranges [b[c], b[c+1]) of a chunked phase A (chunks + 1 entries)."""
+        b = np.zeros(int(chunks) + 1, dtype=np.int64)
+        native.check(native.lib().msbfs_solver_hybrid_chunk_bounds(
+            self._h, int(part), int(nparts), int(n_eff), int(chunks), native.ptr(b, C.c_int64)))
+        return b
+
+    def hybrid_phase_a_chunked(self, queries: QuerySet, part: int, nparts: int, n_eff: int,
+                               count_l1: bool, wbeg: np.ndarray, send_ptr: int, chunks: int,
+                               on_chunk, stream: Optional[int] = None):
+        """hybrid_phase_a with the overlapped exchange: after each own-vertex range's words are
+        packed (enqueued on the solver's stream), on_chunk(c, i0, i1) is called on this thread
+        to start that piece of the all-to-all. Returns (out[2K+3], stats)."""
+        K = queries.K
+        wbeg = np.ascontiguousarray(wbeg, dtype=np.int32)
+        out = np.zeros(2 * K + 3, dtype=np.int64)
+        st = native.Stats()
+        err = []
+
+        def cb(_user, c, i0, i1):
+            if err:
+                return
+            try:
+                on_chunk(int(c), int(i0), int(i1))
+            except BaseException as e:  # noqa: BLE001 (re-raised after the native call)
+                err.append(e)
+
+        fn = native.ChunkFn(cb)  # (kept alive for the call)
+        rc = native.lib().msbfs_solver_hybrid_phase_a_chunked(
+            self._h, K, native.ptr(queries.off, C.c_int64), native.ptr(queries.ids, C.c_int32),
+            int(part), int(nparts), int(n_eff), int(bool(count_l1)), native.ptr(wbeg, C.c_int32),
+            C.c_void_p(send_ptr), native.ptr(out, C.c_int64), int(chunks), fn, None,
+            C.byref(st), C.c_void_p(stream) if stream else None)
+        if err:
+            raise err[0]
+        native.check(rc)
+        return out, st.as_dict()
+
     def hybrid_decode(self, coded_ptr: int, coded_len: np.ndarray, nparts: int, n_eff: int,
                       w_count: int, dense_ptr: int, stream: Optional[int] = None) -> None:
         """Expand the received coded segments (coded_len[r] u64 from each part r, back to back)

@@ -32,6 +32,10 @@ class MsbfsError(RuntimeError):
     pass
 
 
+# void (*)(void* user, int chunk, int64_t i0, int64_t i1): one range of a chunked hybrid phase A
+ChunkFn = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int64, C.c_int64)
+
+
 class Stats(C.Structure):
     _fields_ = [("levels", C.c_int64), ("td_levels", C.c_int64), ("bu_levels", C.c_int64),
                 ("batches", C.c_int64), ("device_ms", C.c_double)]
@@ -116,6 +120,12 @@ def _sig(lib):
                                                         i64p, i64p, P(Stats), vp]),
         "msbfs_solver_hybrid_decode": (C.c_int, [vp, vp, i64p, C.c_int, C.c_int64, C.c_int, vp,
                                                  vp]),
+        "msbfs_solver_hybrid_chunk_bounds": (C.c_int, [vp, C.c_int, C.c_int, C.c_int64, C.c_int,
+                                                       i64p]),
+        "msbfs_solver_hybrid_phase_a_chunked": (C.c_int, [vp, C.c_int64, i64p, i32p, C.c_int,
+                                                          C.c_int, C.c_int64, C.c_int, i32p, vp,
+                                                          i64p, C.c_int, ChunkFn, vp, P(Stats),
+                                                          vp]),
         "msbfs_solver_hybrid_phase_c": (C.c_int, [vp, C.c_int64, C.c_int, C.c_int, C.c_int,
                                                   C.c_int64, vp, i64p, i64p, P(Stats), vp]),
     }

@@ -147,6 +147,13 @@ def unpack_np(recv: np.ndarray, n: int, n_eff: int, nparts: int, nw: int) -> np.
     return rows
 
 
+def torch_sync(device) -> None:
+    """Host wait for everything queued on the device's current stream (the native kernels run
+    on the same null stream; collective pieces were made visible to it by Work.wait())."""
+    import torch
+    torch.cuda.current_stream(device).synchronize()
+
+
 @dataclass
 class HybridResult:
     idx: np.ndarray          # global indices of this rank's groups
@@ -154,10 +161,38 @@ class HybridResult:
     stats: dict = field(default_factory=dict)
 
 
+# Own-vertex ranges of the overlapped exchange (RCCL, dense layout): phase A hands each range's
+# words to the all-to-all as soon as its level-2 pulls are done, while the next range computes.
+DEFAULT_CHUNKS = 4
+
+
+def chunk_views(send, recv, cnt: int, wbeg: np.ndarray, rank: int, pcounts, bounds: np.ndarray,
+                c: int):
+    """(input list, output list) of chunk c for all_to_all: to rank j the words of own vertices
+    [bounds[rank, c], bounds[rank, c+1]) from j's word block of send (destination-major); from
+    rank r its range c, straight into r's block of recv (source-major, the layout phase C reads).
+    bounds[r] are rank r's chunk bounds (every rank's, agreed at setup)."""
+    P = len(wbeg) - 1
+    nw_me = int(wbeg[rank + 1] - wbeg[rank])
+    i0, i1 = int(bounds[rank, c]), int(bounds[rank, c + 1])
+    ins, outs = [], []
+    for j in range(P):
+        nwj = int(wbeg[j + 1] - wbeg[j])
+        base = cnt * int(wbeg[j])
+        ins.append(send[base + i0 * nwj: base + i1 * nwj])
+    rbase = 0
+    for r in range(P):
+        a, b = int(bounds[r, c]), int(bounds[r, c + 1])
+        outs.append(recv[rbase + a * nw_me: rbase + b * nw_me])
+        rbase += int(pcounts[r]) * nw_me
+    return ins, outs
+
+
 class HybridRunner:
     """Reusable buffers + plan for one (solver, K, world) combination."""
 
-    def __init__(self, solver, K: int, ctx: D.DistContext, coded: Optional[bool] = None):
+    def __init__(self, solver, K: int, ctx: D.DistContext, coded: Optional[bool] = None,
+                 chunks: Optional[int] = None):
         import torch
 
         self.solver, self.K, self.ctx = solver, int(K), ctx
@@ -182,6 +217,18 @@ class HybridRunner:
         self._staged = ctx.distributed and ctx.backend != "nccl"
         self.last_bytes = (0, 0)  # (sent, received) of the last exchange
         solver.prepare_hybrid(ctx.rank, ctx.world)  # (phase A's tables, outside timed runs)
+        # overlapped exchange: device collectives (RCCL) and the dense layout only (gloo stages
+        # through host memory, the coded segments exist only once the whole phase A is done)
+        if chunks is None:
+            chunks = DEFAULT_CHUNKS if (ctx.distributed and not self._staged and not self.coded) else 1
+        self.chunks = max(1, int(chunks)) if not (self.coded or self._staged) else 1
+        self.pcounts = [part_count(self.n_eff, r, ctx.world) for r in range(ctx.world)]
+        self.bounds = None
+        if self.chunks > 1:
+            b = solver.hybrid_chunk_bounds(ctx.rank, ctx.world, self.n_eff, self.chunks)
+            full = np.zeros((ctx.world, self.chunks + 1), dtype=np.int64)
+            full[ctx.rank] = b
+            self.bounds = D.allreduce_sum_i64(full.reshape(-1), ctx).reshape(ctx.world, -1)
 
     def _all_to_all(self, recv, send, rsz, ssz) -> None:
         import torch
@@ -224,9 +271,27 @@ class HybridRunner:
             return D.checked(fn, ctx, what) if checked else fn()
 
         t0 = time.perf_counter()
-        out, sa = local(lambda: self.solver.hybrid_phase_a(
-            queries, ctx.rank, P, self.n_eff, ctx.rank == 0, self.wbeg, self.send.data_ptr(),
-            coded=self.coded), "hybrid phase A")
+        works = []
+        if self.chunks > 1:
+            cnt = self.pcounts[ctx.rank]
+
+            def on_chunk(c, i0, i1):  # starts piece c on the collective's stream (async)
+                ins, outs = chunk_views(self.send, self.recv, cnt, self.wbeg, ctx.rank,
+                                        self.pcounts, self.bounds, c)
+                if ctx.distributed:
+                    import torch.distributed as dist
+                    works.append(dist.all_to_all(outs, ins, async_op=True))
+                else:
+                    for o, x in zip(outs, ins):
+                        o.copy_(x)
+
+            out, sa = local(lambda: self.solver.hybrid_phase_a_chunked(
+                queries, ctx.rank, P, self.n_eff, ctx.rank == 0, self.wbeg,
+                self.send.data_ptr(), self.chunks, on_chunk), "hybrid phase A")
+        else:
+            out, sa = local(lambda: self.solver.hybrid_phase_a(
+                queries, ctx.rank, P, self.n_eff, ctx.rank == 0, self.wbeg, self.send.data_ptr(),
+                coded=self.coded), "hybrid phase A")
         t1 = time.perf_counter()  # (phase A returns host sums: its kernels are done)
         if self.coded:
             # one SUM all-reduce: phase-A partial sums + the P x P matrix of coded lengths
@@ -240,6 +305,13 @@ class HybridRunner:
             self._all_to_all(self.rcoded, self.send, rsz, ssz)
             self.solver.hybrid_decode(self.rcoded.data_ptr(), np.array(rsz, np.int64), P,
                                       self.n_eff, self.nw, self.recv.data_ptr())
+        elif self.chunks > 1:
+            ssz, rsz = self.send_sizes, self.recv_sizes
+            reduced = self._allreduce(out.copy())
+            for w in works:  # (the pieces started during phase A)
+                w.wait()
+            if self.recv.is_cuda:
+                torch_sync(self.recv.device)
         else:
             ssz, rsz = self.send_sizes, self.recv_sizes
             reduced = self._allreduce(out.copy())
@@ -258,7 +330,7 @@ class HybridRunner:
                  "phase_a_wall_ms": (t1 - t0) * 1e3, "exchange_ms": (t2 - t1) * 1e3,
                  "phase_c_wall_ms": (t3 - t2) * 1e3,
                  "part": (ctx.rank, P, self.n_eff), "words": self.nw,
-                 "sent_bytes": self.last_bytes[0], "coded": self.coded}
+                 "sent_bytes": self.last_bytes[0], "coded": self.coded, "chunks": self.chunks}
         return HybridResult(self.idx, F, stats)
 
 
@@ -268,13 +340,26 @@ def hybrid_bfs(solver, queries, ctx: Optional[D.DistContext] = None) -> HybridRe
     return HybridRunner(solver, queries.K, ctx).run(queries)
 
 
+def overlapped_exchange_ms(phase_a_ms: float, ready_ms, piece_bytes, gbps: float) -> float:
+    """When the last piece of a rank's chunked exchange has left (ms after its phase A started):
+    piece c can start once it is packed (ready_ms[c]) and the link is free; pieces go one after
+    another at gbps. (Dense, non-chunked: one piece ready at phase_a_ms.)"""
+    t = 0.0
+    for r, b in zip(ready_ms, piece_bytes):
+        t = max(t, r) + b / (gbps * 1e9) * 1e3
+    return max(t, 0.0)
+
+
 def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
-                  coded: Optional[bool] = None) -> np.ndarray:
+                  coded: Optional[bool] = None, chunks: int = 1) -> np.ndarray:
     """Run the hybrid algorithm for `world` ranks sequentially in ONE process on one GPU (no
     torch.distributed): phase A of every rank, a host-side all-to-all, phase C of every rank.
     Returns the full F vector. Used by the GPU tests and to time per-rank phases: with
-    `timings` (a list) one dict per rank is appended (phase A / C device ms, send/recv bytes).
-    coded: zero-word coded exchange (default: coding_default()), decoded on the GPU."""
+    `timings` (a list) one dict per rank is appended (phase A / C device ms and host wall ms,
+    send/recv bytes). coded: zero-word coded exchange (default: coding_default()), decoded on the
+    GPU. chunks > 1 (dense only): phase A runs chunked like the overlapped exchange of
+    HybridRunner; each piece's ready time (CUDA events after its pack) and bytes are recorded
+    ("pieces") so that tools/hybrid_sim.py can price only the exchange phase A does not hide."""
     import torch
 
     coded = coding_default() if coded is None else bool(coded)
@@ -284,12 +369,31 @@ def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
     wbeg = word_split(K, world)
     dev = torch.device("cuda", g.device)
     sends, outs, lens = [], [], []
+    chunks = 1 if coded else max(1, int(chunks))
     for r in range(world):
         ss, rs = split_sizes(n_eff, wbeg, r)
         nb = sum(coded_bound(x) for x in ss) if coded else sum(ss)
         buf = torch.empty(max(1, nb), dtype=torch.int64, device=dev)
-        out, sa = solver.hybrid_phase_a(queries, r, world, n_eff, r == 0, wbeg, buf.data_ptr(),
-                                        coded=coded)
+        pieces = []
+        torch.cuda.synchronize(dev)
+        tw = time.perf_counter()
+        if chunks > 1:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+
+            def on_chunk(c, i0, i1):
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                pieces.append((e, 8 * (i1 - i0) * int(wbeg[-1])))
+
+            out, sa = solver.hybrid_phase_a_chunked(queries, r, world, n_eff, r == 0, wbeg,
+                                                    buf.data_ptr(), chunks, on_chunk)
+            torch.cuda.synchronize(dev)
+            pieces = [(ev0.elapsed_time(e), b) for e, b in pieces]
+        else:
+            out, sa = solver.hybrid_phase_a(queries, r, world, n_eff, r == 0, wbeg,
+                                            buf.data_ptr(), coded=coded)
+        wall_a = (time.perf_counter() - tw) * 1e3
         cl = [int(x) for x in sa["coded_len"]] if coded else list(ss)
         dense = buf[:sum(ss)].cpu().numpy().view(np.uint64) if not coded else None
         sends.append(buf[:sum(cl)].cpu().numpy().view(np.uint64))
@@ -303,7 +407,8 @@ def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
             else:
                 zero = int(len(dense) - np.count_nonzero(dense))
             timings.append({"rank": r, "vertices": part_count(n_eff, r, world),
-                            "phase_a_ms": sa["device_ms"], "send_bytes": 8 * sum(cl),
+                            "phase_a_ms": sa["device_ms"], "phase_a_wall_ms": wall_a,
+                            "pieces": pieces, "send_bytes": 8 * sum(cl),
                             "dense_send_bytes": 8 * sum(ss), "recv_bytes": 0,
                             "send_zero_frac": zero / max(1, sum(ss)), "phase_c_ms": 0.0})
     reduced = np.sum(outs, axis=0)
@@ -333,9 +438,12 @@ def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
             if timings is not None:  # wall time of the GPU decode (launches + kernels)
                 timings[len(timings) - world + j]["decode_ms"] = (time.perf_counter() - t0) * 1e3
             rt = dense
+        torch.cuda.synchronize(dev)
+        tw = time.perf_counter()
         Fc, sc = solver.hybrid_phase_c(K, int(wbeg[j]), nw, world, n_eff, rt.data_ptr(), reduced)
         if timings is not None:
             timings[len(timings) - world + j]["phase_c_ms"] = sc["device_ms"]
+            timings[len(timings) - world + j]["phase_c_wall_ms"] = (time.perf_counter() - tw) * 1e3
             timings[len(timings) - world + j]["levels_c"] = sc["levels"]
         idx = own_groups(K, wbeg, j)
         F[idx] = reduced[idx] + Fc[:len(idx)]

@@ -189,3 +189,32 @@ def test_cli_gpu_many_passes_drain(tmp_path, msbfs_pkg, ranks, comm):
               "--async-slots", "2", "--repeat", "2", "--json"])
     js = _check(r, ref, m, ranks)
     assert js["comm"] == comm
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+@pytest.mark.parametrize("ranks,comm,chunks", [(2, "mpi", 3), (3, "mpi", 2), (1, "rccl", 4),
+                                               (1, "rccl", 0)])
+def test_cli_gpu_hybrid_chunked_exchange(tmp_path, msbfs_pkg, ranks, comm, chunks):
+    """--chunks N: the overlapped hybrid exchange (phase A hands out its vertex ranges, one
+    all-to-all piece each; RCCL: grouped send/recv on the communicator's stream while phase A
+    goes on; host MPI: staged pieces). chunks 0 = the default (4 with RCCL)."""
+    m = msbfs_pkg
+    g, qs, gp, qp = _files(tmp_path, m, 300, 4)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    r = _run([MPIEXEC, "-n", str(ranks), _cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo",
+              "bitpar", "--dist", "hybrid", "--comm", comm, "--chunks", str(chunks), "--repeat",
+              "2", "--json"])
+    js = _check(r, ref, m, ranks)
+    assert js["comm"] == comm
+
+
+def test_cli_gpu_spmd_hybrid_chunked(tmp_path, msbfs_pkg):
+    """--spmd 3 threads (ThreadComm) with the chunked hybrid exchange: every piece staged through
+    the in-process collectives, in the same order on every thread."""
+    m = msbfs_pkg
+    g, qs, gp, qp = _files(tmp_path, m, 300, 4)
+    ref = m.cpu_bfs(g, qs, count_edges=True)
+    r = _run([_cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo", "bitpar", "--spmd", "3",
+              "--dist", "hybrid", "--chunks", "3", "--json"], {"MSBFS_NO_MPI": "1"})
+    js = _check(r, ref, m, 3)
+    assert js["comm"] == "threads"

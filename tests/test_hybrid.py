@@ -272,7 +272,39 @@ def test_hybrid_tiled_phase_a(msbfs_pkg):
         assert np.array_equal(s.run(qs).F, ref)
         for world in (2, 3, 8, 2):
             assert np.array_equal(H.emulate_ranks(s, qs, world), ref), world
+        # the overlapped exchange: phase A's tiled level 2 in vertex ranges, each packed as soon
+        # as it is final (the pieces' ready times are recorded, in order)
+        for world, chunks in ((8, 4), (3, 7), (1, 2)):
+            tim = []
+            assert np.array_equal(H.emulate_ranks(s, qs, world, timings=tim, chunks=chunks),
+                                  ref), (world, chunks)
+            for x in tim:
+                ready = [p[0] for p in x["pieces"]]
+                assert len(ready) == chunks and ready == sorted(ready)
+                assert sum(p[1] for p in x["pieces"]) == x["dense_send_bytes"]
+            b = s.hybrid_chunk_bounds(0, world, dg.hybrid_extent(), chunks)
+            assert b[0] == 0 and b[-1] == H.part_count(dg.hybrid_extent(), 0, world)
+            assert np.all(np.diff(b) >= 0) and len(b) == chunks + 1
     dg.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,chunks", [(4, 3), (2, 5), (8, 2)])
+def test_hybrid_chunked_small_graph(msbfs_pkg, world, chunks):
+    """Chunked phase A on a graph too small for the tiled pull: the ranges are packed and handed
+    out after the level (same callbacks, same answers)."""
+    m = msbfs_pkg
+    H = _H()
+    dg = m.DeviceGraph.rmat(14, 16, 3, device=0, relabel=True)
+    qs = m.QuerySet.random(dg.n, 700, 8, seed=9)
+    with m.Solver(dg, "bitpar", max_groups=1024) as s:
+        ref = s.run(qs).F
+        tim = []
+        assert np.array_equal(H.emulate_ranks(s, qs, world, timings=tim, chunks=chunks), ref)
+        assert all(len(x["pieces"]) == chunks for x in tim)
+        # one process, HybridRunner's own chunked path (local copies per piece)
+        r = H.HybridRunner(s, qs.K, H.D.DistContext(device=0), chunks=chunks).run(qs)
+        assert np.array_equal(r.F, ref) and r.stats["chunks"] == chunks
 
 
 @pytest.mark.gpu
