@@ -469,11 +469,15 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
 // go to an overflow list (ctr->touched, unused by pull levels) that k_bu_narrow then processes
 // from scratch.
 // ---------------------------------------------------------------------------------------------
+// dsnap / skip (tuning dskip, see k_bu_full): a first neighbour done at the level start
+// covers every alive group (probe instead of its row); every vertex this pass finishes is done,
+// so with skip it writes no row at all.
 template <int W>
 __global__ __launch_bounds__(kBlock, 8) void k_bu_first(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
-    int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF, const int32_t* first) {
+    int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF, const int32_t* first,
+    const uint32_t* dsnap, int skip) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   // done / any-visited bits: one atomic per word of the wave (wave_set_bits) where a wave
@@ -508,7 +512,9 @@ __global__ __launch_bounds__(kBlock, 8) void k_bu_first(
       const int32_t u = first ? first[v] : col[rowptr[v]];  // active vertices have deg > 0
       r = ldv<VW>(R + (int64_t)v * W + slot * VW);
       deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);  // only counted, off the load chain
-      const V<VW> x = ldv<VW>(R + (int64_t)u * W + slot * VW);
+      V<VW> x;
+      if (dsnap && ((dsnap[u >> 5] >> (u & 31)) & 1u)) x = am;  // (a done first neighbour)
+      else x = ldv<VW>(R + (int64_t)u * W + slot * VW);
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
         const uint64_t unv = ~r.w[j] & am.w[j];
@@ -520,7 +526,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_bu_first(
     const bool g_open = (__ballot(open) >> (sub * G)) & L::GBITS;
     const bool fin = valid && !g_open;  // covered by the first row: finished at this level
     if (!fin) nw = vzero<VW>();
-    if (fin) {
+    if (fin && !skip) {
       V<VW> nv;
 #pragma unroll
       for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
@@ -583,7 +589,7 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
                                            const uint32_t* hub, int32_t filter_from, int coop,
                                            int32_t* lst, const uint32_t* code,
                                            int32_t code_from, unsigned long long* wacc,
-                                           const uint32_t* snap) {
+                                           const uint32_t* snap, const uint32_t* dsnap) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, S = L::VPW;
   constexpr int PB = VW == 2 ? 4 : 8;  // rows in flight per lane group in phase B
@@ -642,6 +648,18 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
 #pragma unroll
       for (int q = 0; q < Q; ++q)
         if (u[q] >= 0 && !(((pg[q] & ph[q]) >> (u[q] & 31)) & 1u)) u[q] = -1;
+    }
+    if (dsnap) {  // (uniform) done neighbours: the alive mask instead of their rows (k_bu_full)
+      bool hit = false;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (u[q] >= 0 && ((dsnap[u[q] >> 5] >> (u[q] & 31)) & 1u)) {
+          u[q] = -1;
+          hit = true;
+        }
+      if (__ballot(hit))
+#pragma unroll
+        for (int j = 0; j < VW; ++j) a.w[j] |= am.w[j];
     }
     if (code_from != kNoCodes) {  // wave-uniform
       // single-group neighbours: their bit goes into this wave's LDS words (ds_or_b64) instead
@@ -824,7 +842,7 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const uint64_t* R,
     const uint64_t* alive, const uint64_t* gmask, uint64_t* acc, const uint32_t* anyvis,
     int32_t filter_from, int coop, const uint32_t* code, int32_t code_from,
-    const uint32_t* snap) {
+    const uint32_t* snap, const uint32_t* dsnap = nullptr) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G;
   __shared__ int32_t tile[BT / 64][T];
@@ -858,7 +876,7 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const int64_t lim = beg + uni32(d.len);
     if (c + cstep < cend) d = desc[c + cstep];  // next descriptor, in flight during the pull
     chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop,
-                           lst, code, code_from, wacc[threadIdx.x >> 6], snap);
+                           lst, code, code_from, wacc[threadIdx.x >> 6], snap, dsnap);
   }
 }
 

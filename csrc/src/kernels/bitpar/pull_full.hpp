@@ -116,15 +116,27 @@ __device__ __forceinline__ void wq_flush(int32_t* q, uint32_t& n, int32_t* out, 
   n = 0;
 }
 
+// Done rows are never read (tuning key dskip, BitparSolver::level_bu): a vertex that is done (every
+// alive group visited) has every group alive now, so a pull may OR the alive mask instead of its
+// row. dsnap = the done bitmap as of the level start (a vertex done during this level may hold
+// bits of this level; its row of the previous level is still valid and is read); a neighbour
+// done in dsnap is probed (4 bytes) instead of gathered (8*W bytes), and with `skip` a vertex
+// finishing at this level does not write its row at all (RMAT-26 levels 3-4: ~32M rows). The
+// one reader that needs such a row, a push level right after, gets it from k_fix_done_rows.
+__device__ __forceinline__ bool done_in(const uint32_t* snap, int32_t u) {
+  return u >= 0 && ((snap[u >> 5] >> (u & 31)) & 1u);
+}
+
 // CS neighbours per step; C1 > 0: a first step of only C1 rows (late levels are mostly covered by
 // the first neighbour, rows sorted hubs first). nact_dev: list length on the device (device-driven
-// levels). gate: closed levels of a device-driven batch are no-ops.
+// levels). gate: closed levels of a device-driven batch are no-ops. dsnap / skip: see above.
 template <int W, int CS = 8, int C1 = 0>
 __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, int64_t n, const uint64_t* alive, const uint64_t* gmask,
     uint32_t* done, int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* actw2,
-    int next_wide, uint32_t* slabF, const uint32_t* nact_dev, BuGate gate) {
+    int next_wide, uint32_t* slabF, const uint32_t* nact_dev, BuGate gate,
+    const uint32_t* dsnap, int skip) {
   if (!bu_gate_open(gate)) return;  // (uniform)
   if (nact_dev) nact = (int64_t)*nact_dev;
   using L = Lay<W>;
@@ -213,6 +225,18 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
     if (g_open) {
       // first step: the preloaded ids (F1 of them)
       {
+        if (dsnap) {  // (uniform) done neighbours: the alive mask instead of their rows
+          bool hit = false;
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (done_in(dsnap, u0[q])) {
+              u0[q] = -1;
+              hit = true;
+            }
+          if ((__ballot(hit) >> (sub * G)) & L::GBITS)
+#pragma unroll
+            for (int j = 0; j < VW; ++j) acc.w[j] = am.w[j];
+        }
         int32_t uc[F1];
         bcast_ids<G, Q, F1>(u0, uc, std::make_integer_sequence<int, F1>{});
         V<VW> x[F1];
@@ -233,6 +257,18 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
         for (int q = 0; q < Q; ++q) {
           const int64_t ee = e + q * G + slot;
           u[q] = ee < end ? col[ee] : -1;
+        }
+        if (dsnap) {
+          bool hit = false;
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (done_in(dsnap, u[q])) {
+              u[q] = -1;
+              hit = true;
+            }
+          if ((__ballot(hit) >> (sub * G)) & L::GBITS)
+#pragma unroll
+            for (int j = 0; j < VW; ++j) acc.w[j] |= am.w[j];
         }
         int32_t uc[C];
         bcast_ids<G, Q, C>(u, uc, std::make_integer_sequence<int, C>{});
@@ -258,20 +294,21 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
       anynew |= nwv.w[j] != 0;
       notfull |= (unv.w[j] & ~nwv.w[j]) != 0;
     }
+    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
+    const bool g_new = (bn >> (sub * G)) & L::GBITS;
+    const bool g_nf = (bf >> (sub * G)) & L::GBITS;
     {  // also when nothing is open: Wb may hold the previous batch's rows (invalid lanes: index -1)
+      // (skip: a vertex done now is never read again, see above)
       V<VW> nv;
 #pragma unroll
       for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nwv.w[j];
-      st_row<VW>(rO, valid ? v : -1, voff, nv);
+      st_row<VW>(rO, valid && (g_nf || !skip) ? v : -1, voff, nv);
     }
     bc.add(nwv);  // (zero for invalid lanes)
     if (++nadd == (1 << BitCounter<VW>::D) - 1) {
       bc.template spill_strided<CR>(cnt, slot);
       nadd = 0;
     }
-    const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
-    const bool g_new = (bn >> (sub * G)) & L::GBITS;
-    const bool g_nf = (bf >> (sub * G)) & L::GBITS;
     const bool leader = valid && slot == 0;
     wave_set_bits<kCombine>(done, v, leader && !g_nf);
     const bool keep = leader && g_nf, app = leader && g_new;
@@ -303,6 +340,35 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
   __syncthreads();
   uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
   for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
+}
+
+// A push level after a pull level that skipped the rows of its finishing vertices (dskip) reads
+// the frontier's new bits as Wrow & ~Rrow: restore Wrow[v] = Rrow[v] | am for the frontier
+// vertices that finished (done) at that level (their new bits were exactly am & ~Rrow[v]).
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_fix_done_rows(const int32_t* fl, const uint32_t* nf_dev,
+                                                          int64_t nf, const uint32_t* done,
+                                                          const uint64_t* Rrow, uint64_t* Wrow,
+                                                          const uint64_t* alive,
+                                                          const uint64_t* gmask) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  if (nf_dev) nf = (int64_t)*nf_dev;
+  const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nf; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t i = tb + wv * VPW + sub;
+    if (i >= nf) continue;
+    const int32_t v = fl[i];
+    if (!is_done(done, v)) continue;
+    const int64_t o = (int64_t)v * W + slot * VW;
+    V<VW> r = ldv<VW>(Rrow + o);
+#pragma unroll
+    for (int j = 0; j < VW; ++j) r.w[j] |= am.w[j];
+    stv<VW>(Wrow + o, r);
+  }
 }
 
 }  // namespace bp

@@ -82,6 +82,10 @@ struct Tuning {
   // k_bu_full (structured-buffer rows, wave-private list queues; bitpar/pull_full.hpp) instead
   // of k_bu_narrow
   int full = 1;
+  // done rows are never read (k_bu_full): pulls probe a level-start snapshot of the done bitmap
+  // instead of gathering done neighbours' rows, and the rows of vertices finishing on an
+  // unfiltered pull level are not written (a push level right after gets them restored)
+  int dskip = 1;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->
   // 12: 13.85 -> 13.32 ms)
@@ -149,6 +153,11 @@ class BitparSolver final : public Solver {
     std::vector<int64_t> chunk_b;
     std::function<void(int)> on_chunk;
     int chunks_done = 0;
+    // dskip: the last level skipped the rows of the vertices it finished; a push level next
+    // restores those of its frontier (k_fix_done_rows) from the read buffer and this alive mask
+    bool keep_rows = false;             // every row written (hybrid phase A packs them)
+    bool skip_pending = false;
+    const uint64_t* skip_alive = nullptr;
   };
   struct Small {
     unsigned long long* F;
@@ -323,6 +332,11 @@ class BitparSolver final : public Solver {
   std::vector<std::unique_ptr<TileSet>> tilesets_;  // per vertex partition (hybrid emulation: all)
   bool tiles_ok_ = true;  // false once the tiles did not fit
   DevBuf fbm_tile_, lcnt_, zrow_;  // frontier bitmap of a tiled level, list counter, zero row
+  DevBuf dsnap_;                   // done bitmap as of a dskip level's start
+  // dskip for the next pull level: snapshot of the done bitmap (nullptr: off for this level)
+  const uint32_t* done_snapshot(const Loop& S, bool unfiltered, hipStream_t s);
+  template <int W>
+  void fix_done_rows(Loop& S, hipStream_t s);
   int num_cus_ = 0;
   DevBuf bctr_;  // (kBatch+1) Ctr slots, then (kBatch+1) x 16 alive words
   std::unique_ptr<PinnedBuf> hbctr_;

@@ -162,6 +162,7 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
   S.weight_l1 = count_l1;
   S.plan = "TB";
   S.lazy = tun_.lazy && opt.force_dir == 0 && tun_.dirs.empty();
+  S.keep_rows = true;  // (every own row is packed after level 2)
   const int wt = (int)((K + 63) / 64);
   const WordSplit ws = word_split(wbeg, nparts, wt);
   // pack own-vertex range [i0, i1) of buffer vis into its place in send

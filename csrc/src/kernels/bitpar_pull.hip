@@ -101,6 +101,30 @@ void BitparSolver::prepare(hipStream_t s) {
   (void)ne;
 }
 
+// dskip (see pull_full.hpp): the done bitmap as of this level's start, for the unfiltered pull
+// levels (a filtered level never follows one in a batch: ev only grows; not in hybrid phase A,
+// which packs the rows; not in the edge-counting pass)
+const uint32_t* BitparSolver::done_snapshot(const Loop& S, bool unfiltered, hipStream_t s) {
+  if (!tun_.dskip || !tun_.full || S.keep_rows || !unfiltered) return nullptr;
+  const size_t b = (size_t)((g_.n + 31) / 32) * sizeof(uint32_t);
+  dsnap_.ensure(std::max<size_t>(b, 4));
+  MSBFS_HIP_CHECK(hipMemcpyAsync(dsnap_.p, done_.p, b, hipMemcpyDeviceToDevice, s));
+  return dsnap_.as<uint32_t>();
+}
+
+// rows of the last (dskip) pull level's frontier vertices that finished there (see
+// k_fix_done_rows); the level's output buffer is vis_[cur], its input vis_[cur ^ 1]
+template <int W>
+void BitparSolver::fix_done_rows(Loop& S, hipStream_t s) {
+  S.skip_pending = false;
+  if (S.nf <= 0) return;
+  const Small sm = small();
+  k_fix_done_rows<W><<<grid_for(S.nf, Lay<W>::TILE, kMaxGrid), kBlock, 0, s>>>(
+      fl_[S.fc].as<int32_t>(), nullptr, S.nf, done_.as<uint32_t>(),
+      vis_[S.cur ^ 1].as<uint64_t>(), vis_[S.cur].as<uint64_t>(), S.skip_alive, sm.gmask);
+  MSBFS_HIP_CHECK(hipGetLastError());
+}
+
 template <int W, bool COUNT>
 int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   using L = Lay<W>;
@@ -172,6 +196,13 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   // has the LDS to itself, 128 KB (ids < 1M)
   const bool hub_lds = filter_from == 0 && n > (int64_t)kHubW * 32 * 4;
   const bool hub_big = n > (int64_t)kHubBig * 32 * 4;
+  // dskip: probes of done neighbours (and no rows for finishing vertices) on the unfiltered
+  // levels after the first pull level, all of whose kernels probe (k_bu_full, k_bu_first, the
+  // hub chunks); the per-vertex pulls of tun_.full = 0 do not
+  const uint32_t* dsnap =
+      (!COUNT && !tiled) ? done_snapshot(S, filter_from == INT32_MAX && !lazy_first, s) : nullptr;
+  S.skip_pending = dsnap != nullptr;
+  S.skip_alive = alive;
   // counting fused into the traversal kernels (the edge-count pass keeps k_count_frontier)
   constexpr bool FUSE = !COUNT;
   // prefix pull + tail push on the first bottom-up level (see k_push_tail): the pulls stop at
@@ -257,7 +288,8 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
         k_bu_first<W><<<gl, kBlock, 0, s>>>(
             act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
             done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s));
+            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
+            dsnap ? 1 : 0);
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gl;
         if (tun_.full)
@@ -265,7 +297,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
               done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
-              slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{});
+              slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{}, dsnap, dsnap ? 1 : 0);
         else
           k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
@@ -281,7 +313,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                                  sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                  fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                  anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
-                                 slabF<W>(rows), nullptr, BuGate{});
+                                 slabF<W>(rows), nullptr, BuGate{}, dsnap, dsnap ? 1 : 0);
         rows += gn;
       } else {
         auto kn = FUSE ? (filt ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, true>
@@ -333,12 +365,12 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
           desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
           sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-          coop, codes, code_from, snap);
+          coop, codes, code_from, snap, dsnap);
     } else {
       k_bu_chunks<W, 256, kBlock, 0><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
           desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask,
           acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, coop, codes, code_from,
-          snap);
+          snap, dsnap);
     }
     MSBFS_HIP_CHECK(hipGetLastError());
     const int gw = grid_for(S.nactw, L::TILE, grid);
@@ -415,6 +447,14 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
   trace::Range range_batch("bitpar L%u-%u BU batch", level0 + 1, level0 + K);
   auto kn = k_bu_narrow<W, false, kBlock, 0, true, false, false, 8, 1>;
   const bool full = tun_.full != 0;
+  // dskip: every level of the batch snapshots the done bitmap at its start (a copy on the stream,
+  // also for the levels whose gate closes)
+  const bool dsk = full && tun_.dskip && !S.keep_rows;
+  const uint32_t* dsnap = nullptr;
+  if (dsk) {
+    dsnap_.ensure(std::max<size_t>((size_t)((g_.n + 31) / 32) * sizeof(uint32_t), 4));
+    dsnap = dsnap_.as<uint32_t>();
+  }
   auto launch = [&](int grid, const int32_t* list, const uint64_t* R, uint64_t* O,
                     const uint64_t* alive, int32_t* fl_out, Ctr* out, uint32_t* slab,
                     const uint32_t* len, const BuGate& gate, int p) {
@@ -422,7 +462,7 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
       k_bu_full<W, 8, 1><<<grid, kBlock, 0, s>>>(
           list, 0, g_.rowptr, g_.col, R, O, g_.n, alive, sm.gmask, done_.as<uint32_t>(),
           act_[p ^ 1].as<int32_t>(), fl_out, out, anyvis_.as<uint32_t>(),
-          actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate);
+          actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate, dsnap, dsnap ? 1 : 0);
     else
       kn<<<grid, kBlock, 0, s>>>(list, 0, g_.rowptr, g_.col, R, O, alive, sm.gmask,
                                  done_.as<uint32_t>(), act_[p ^ 1].as<int32_t>(), fl_out, out,
@@ -436,6 +476,9 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
     uint64_t* O = vis_[S.cur ^ p ^ 1].as<uint64_t>();
     int32_t* fl_out = fl_[S.fc ^ p ^ 1].as<int32_t>();
     const uint64_t* alive = aslot + 16 * i;
+    if (dsnap)
+      MSBFS_HIP_CHECK(hipMemcpyAsync(dsnap_.p, done_.p, (size_t)((g_.n + 31) / 32) * 4,
+                                     hipMemcpyDeviceToDevice, s));
     launch(gn, act_[p].as<int32_t>(), R, O, alive, fl_out, slots + i + 1, slabF<W>(0),
            &slots[i].act2.v, gate, p);
     if (gw)
@@ -491,11 +534,16 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
   }
   S.fsrc_acc = false;
   S.osnap_next = false;
+  // (the last real level's alive mask stays in bctr_ until the next batch: a push level right
+  // after restores the skipped rows of its frontier first, see levels())
+  S.skip_pending = dsnap && real > 0;
+  S.skip_alive = aslot + 16 * std::max(real - 1, 0);
   // the next batch: twice as long while the frontier lives, else this tail's length + 1
   bu_next_ = real == K ? std::min(2 * K, kBatch) : real + 1;
 }
 
 #define MSBFS_BP_INST(WW)                                                 \
+  template void BitparSolver::fix_done_rows<WW>(Loop&, hipStream_t);     \
   template int BitparSolver::level_bu<WW, false>(Loop&, hipStream_t);    \
   template int BitparSolver::level_bu<WW, true>(Loop&, hipStream_t);     \
   template bool BitparSolver::bu_batch_ok<WW, false>(const Loop&) const; \

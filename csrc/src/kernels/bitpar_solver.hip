@@ -44,13 +44,14 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "tiles") tiles = (int)to_num(key, v);
   else if (key == "tiles_code_deg") tiles_code_deg = to_num(key, v);
   else if (key == "full") full = (int)to_num(key, v);
+  else if (key == "dskip") dskip = (int)to_num(key, v);
   else if (key == "dirs") {
     for (char c : v)
       if (c != 'T' && c != 'B' && c != '.') fail("tuning: dirs takes T, B or . per level");
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip dirs)");
   }
 }
 
@@ -259,6 +260,10 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
     // low-degree graphs (road-like: thousands of small top-down levels): run a batch of levels
     // without host round trips (kernels read the frontier sizes from device counters)
     if (!bottom_up) materialize_frontier(S, s);  // (a tiled pull left only its bitmap)
+    if (!bottom_up && S.skip_pending) {
+      // push after a dskip pull level: restore its frontier's skipped rows
+      fix_done_rows<W>(S, s);
+    }
     if (!bottom_up && tun_.batch > 1 && g_.max_degree <= kSmallDeg && !trace &&
         S.level + 2 < S.stop_level && opt.force_dir != 2 && S.plan.empty() &&
         (dirs.size() <= S.level)) {
