@@ -50,6 +50,7 @@ struct Args {
   int async_slots = 0;  // asynchronous MIN slots before a drain (0: Comm::kAsyncSlots; tests)
   int chunks = 0;       // hybrid: pieces of the overlapped exchange (0: 4 with RCCL, else 1)
   bool cache = false, json = false, sort_rows = false, relabel = true;
+  bool host_csr = false;  // build the CSR of a graph file on the host (default: on the device)
 };
 
 std::vector<std::string> split(const std::string& s, char d) {
@@ -154,7 +155,7 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
       int64_t hdr[3] = {0, 0, 0};  // n, m, CSR already on rank 0's device
       if (comm->rank() == 0) {
         try {
-          if (!cpu && !a.cache) {
+          if (!cpu && !a.cache && !a.host_csr) {
             device_graph_from_edge_file(dg, a.graph, stream);
             hdr[0] = dg.n;
             hdr[1] = dg.m;
@@ -647,6 +648,7 @@ int main(int argc, char* argv[]) {
     else if (!strcmp(argv[i], "--json")) a.json = true;
     else if (!strcmp(argv[i], "--sort-rows")) a.sort_rows = true;
     else if (!strcmp(argv[i], "--no-relabel")) a.relabel = false;
+    else if (!strcmp(argv[i], "--host-csr")) a.host_csr = true;
   }
   int rc = 0;
   if (a.spmd >= 1) {

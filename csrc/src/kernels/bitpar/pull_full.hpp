@@ -178,39 +178,64 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
   int32_t v1 = -1, v2 = -1;
   if (tb + lofs < nact) v1 = act[tb + lofs];
   if (tb + stride + lofs < nact) v2 = act[tb + stride + lofs];
+  // Every prefetch below is an unconditional load from a clamped index (an invalid lane reads
+  // row / offsets / column entry 0) with the result selected after: a load under a branch made
+  // the compiler wait for it at the branch's end (s_waitcnt vmcnt(0) across basic blocks), which
+  // undid the pipeline (round-3 k_bu_narrow waited for its prefetched offsets on the spot).
   V<VW> r1 = ld_row<VW>(rR, v1, voff);  // (v1 = -1: zeros)
-  int64_t b1 = 0;
-  uint32_t d1 = 0;
-  if (v1 >= 0) {
-    b1 = rowptr[v1];
-    d1 = (uint32_t)(rowptr[v1 + 1] - b1);
-  }
+  int64_t b1 = rowptr[v1 >= 0 ? v1 : 0], e1 = rowptr[(v1 >= 0 ? v1 : 0) + 1];
+  if (v1 < 0) e1 = b1;
   constexpr int F1 = C1 > 0 ? C1 : C;  // neighbours of the first step
-  int32_t u1[Q];
+  // column entries [b, b + F1) of a row [b, e): slot q*G + lane's entry, -1 past the end
+  auto first_ids = [&](int64_t b, int64_t e, int32_t (&u)[Q]) {
 #pragma unroll
-  for (int q = 0; q < Q; ++q)
-    u1[q] = (q * G + slot < F1 && (uint32_t)(q * G + slot) < d1) ? col[b1 + q * G + slot] : -1;
+    for (int q = 0; q < Q; ++q) {
+      const int k = q * G + slot;
+      const bool ok = k < F1 && b + k < e;
+      const int32_t x = col[ok ? b + k : 0];
+      u[q] = ok ? x : -1;
+    }
+  };
+  // done-probe words of ids u (a dsnap word; 0 without probes or for -1)
+  auto probe_words = [&](const int32_t (&u)[Q], uint32_t (&pd)[Q]) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) pd[q] = 0u;
+    if (dsnap) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const uint32_t w = dsnap[(u[q] >= 0 ? u[q] : 0) >> 5];
+        pd[q] = u[q] >= 0 ? w : 0u;
+      }
+    }
+  };
+  int32_t u1[Q];
+  uint32_t pd1[Q];  // dsnap words of u1 (the done probe, loaded a tile ahead too)
+  first_ids(b1, e1, u1);
+  probe_words(u1, pd1);
   for (; tb < nact; tb += stride) {
     const int64_t idx = tb + lofs;
     const bool valid = idx < nact;
     const int32_t v = valid ? v1 : 0;
     const V<VW> r = r1;
-    const int64_t beg = b1, end = b1 + d1;
-    const uint32_t deg = d1;
+    const int64_t beg = b1, end = e1;
+    const uint32_t deg = (uint32_t)(e1 - b1);
     int32_t u0[Q];
+    uint32_t pd0[Q];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) u0[q] = u1[q];
+    for (int q = 0; q < Q; ++q) {
+      u0[q] = u1[q];
+      pd0[q] = pd1[q];
+    }
     // prefetch: row / offsets of the next tile, list entry of the one after
     v1 = idx + stride < nact ? v2 : -1;
     r1 = ld_row<VW>(rR, v1, voff);
-    if (v1 >= 0) {
-      b1 = rowptr[v1];
-      d1 = (uint32_t)(rowptr[v1 + 1] - b1);
-    } else {
-      b1 = 0;
-      d1 = 0;
+    b1 = rowptr[v1 >= 0 ? v1 : 0];
+    e1 = rowptr[(v1 >= 0 ? v1 : 0) + 1];
+    {
+      const int64_t i2 = idx + 2 * stride;
+      const int32_t a2 = act[i2 < nact ? i2 : 0];
+      v2 = i2 < nact ? a2 : v2;
     }
-    if (idx + 2 * stride < nact) v2 = act[idx + 2 * stride];
     V<VW> unv = vzero<VW>(), acc = vzero<VW>();
     bool lane_open = false, rnz = false;
     if (valid) {
@@ -222,6 +247,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
       }
     }
     bool g_open = valid && ((__ballot(lane_open) >> (sub * G)) & L::GBITS);
+    const bool g_first_step = g_open;
     if (g_open) {
       // first step: the preloaded ids (F1 of them)
       {
@@ -229,7 +255,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
           bool hit = false;
 #pragma unroll
           for (int q = 0; q < Q; ++q)
-            if (done_in(dsnap, u0[q])) {
+            if (u0[q] >= 0 && ((pd0[q] >> (u0[q] & 31)) & 1u)) {
               u0[q] = -1;
               hit = true;
             }
@@ -242,6 +268,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
         V<VW> x[F1];
 #pragma unroll
         for (int c = 0; c < F1; ++c) x[c] = ld_row<VW>(rR, uc[c], voff);
+        // (the next tile's first-step ids behind the rows: waiting for the rows leaves them in
+        // flight; their offsets were loaded at the top of this tile)
+        if (v1 < 0) e1 = b1;
+        first_ids(b1, e1, u1);
         bool cov = true;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
@@ -256,13 +286,16 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
           const int64_t ee = e + q * G + slot;
-          u[q] = ee < end ? col[ee] : -1;
+          const int32_t x = col[ee < end ? ee : e];
+          u[q] = ee < end ? x : -1;
         }
         if (dsnap) {
+          uint32_t pd[Q];
+          probe_words(u, pd);
           bool hit = false;
 #pragma unroll
           for (int q = 0; q < Q; ++q)
-            if (done_in(dsnap, u[q])) {
+            if (u[q] >= 0 && ((pd[q] >> (u[q] & 31)) & 1u)) {
               u[q] = -1;
               hit = true;
             }
@@ -285,6 +318,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
         // the group runs this loop in lock step (same v); it stops when all its lanes are covered
         g_open = (__ballot(!cov) >> (sub * G)) & L::GBITS;
       }
+    }
+    if (!g_first_step) {  // (no first step ran for this group: the next tile's ids now)
+      if (v1 < 0) e1 = b1;
+      first_ids(b1, e1, u1);
     }
     V<VW> nwv;
     bool anynew = false, notfull = false;
@@ -319,10 +356,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
       wave_set_bits<kCombine>(anyvis, v, leader && g_first);
       if (leader && g_first) ev += deg;
     }
-    // third stage: the next tile's first-step ids (its offsets arrived during this tile)
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-      u1[q] = (q * G + slot < F1 && (uint32_t)(q * G + slot) < d1) ? col[b1 + q * G + slot] : -1;
+    // third stage: the done probe of the next tile's first-step ids (loaded during this tile)
+    probe_words(u1, pd1);
     wq_push(qa, na, keep && (int)deg <= next_wide, v);
     wq_push(qw, nw, keep && (int)deg > next_wide, v);
     wq_push(qf, nf, app, v);

@@ -542,3 +542,31 @@ def test_dist_device_batches_and_reset(msbfs_pkg):
                     assert np.array_equal(r.F, ref.F), (gi, algo)
                     assert np.array_equal(r.edges, ref.edges), (gi, algo)
         dg.close()
+
+
+@pytest.mark.parametrize("dirs", ["", "TBBTBBTBBTBBTBBT", "TBTBTBTBTBTBTBTB", "TBBBBBBBBBBBBBBT"])
+@pytest.mark.parametrize("extra", [{}, {"lean_min": 0}, {"bu_max": 1 << 30}, {"full": 0}])
+def test_bitpar_done_rows_skipped(msbfs_pkg, dirs, extra):
+    """dskip (round 4): unfiltered pull levels never read done vertices' rows (a level-start
+    snapshot of the done bitmap is probed, the alive mask ORed) and write none for the vertices
+    they finish; a push level right after restores the skipped rows of its frontier. Forced
+    pull -> push -> pull plans, the lean pass (lean_min=0), device-driven pull batches and the old
+    per-vertex pulls (full=0: no skipping) all give the oracle's F, dskip on and off, over
+    several batches and a reused solver."""
+    m = msbfs_pkg
+    dg = m.DeviceGraph.rmat(14, 16, 5, device=0)
+    hg = dg.download()
+    dg.relabel_by_degree()
+    cases = [(dg, hg, 1024), (dg, hg, 1500), (dg, hg, 100)]
+    for name, g in _graphs(m)[2:4]:
+        cases.append((g.to_device(0), g, 300))
+    for dev, host, K in cases:
+        qs = m.QuerySet.random(host.n, K, 5, seed=K + 3)
+        ref = m.cpu_bfs(host, qs)
+        for dskip in (1, 0):
+            tun = dict(extra, dskip=dskip)
+            if dirs:
+                tun["dirs"] = dirs
+            with m.Solver(dev, "bitpar", max_groups=min(K, 1024), tuning=tun) as s:
+                assert np.array_equal(s.run(qs).F, ref.F), (dirs, extra, K, dskip)
+                assert np.array_equal(s.run(qs).F, ref.F), (dirs, extra, K, dskip)

@@ -8,7 +8,10 @@ legacy binary edge list, against the device-generator path (--gen, no file at al
 Writes a Graph500 RMAT edge list in the reference's format (int32 n, int64 m, m x (int32, int32);
 8.6 GB at scale 26) and a query file (extended format for K > 255), then runs the drop-in CLI
 (`_bin/msbfs -g G -q Q -gn 1`) cold and warm, with and without the CSR sidecar cache (--cache:
-the first run writes it, the second reads it), and with --gen. Prints one JSON line per run and
+the first run writes it, the second reads it), and with --gen. The plain file runs build the CSR
+on the device (the mapped edge list streamed to HBM, device count / scan / scatter);
+--host-csr is the host build of rounds 1-3 for comparison. "cold" is the first read after the
+file was written (the page cache is not dropped: that needs root). Prints one JSON line per run and
 a summary; the answers (minimum group, F) must agree across every run.
 """
 from __future__ import annotations
@@ -85,7 +88,7 @@ def main() -> int:
     cli = native.CLI_PATH
     env = dict(os.environ, MSBFS_NO_MPI="1")
     base = ["-g", gpath, "-q", qpath, "-gn", "1"]
-    runs = [("file_cold", base), ("file_warm", base),
+    runs = [("file_cold", base), ("file_warm", base), ("file_host_csr", base + ["--host-csr"]),
             ("cache_build", base + ["--cache"]), ("cache_read", base + ["--cache"]),
             ("gen", ["--gen", f"rmat:{args.scale}:{args.edgefactor}:1", "--qgen",
                      f"{args.groups}:{args.group_size}:7", "-gn", "1"])]
