@@ -6,10 +6,14 @@
 // every neighbour row): G lanes per vertex, CS neighbours per step, early exit once every alive
 // group is covered. Round-4 changes, from the level-3 ISA and counters of k_bu_narrow (5.6 ms,
 // 3.0 TB/s, ~310 VALU per tile, six block barriers per tile):
-//  * rows move with STRUCTURED buffer loads / stores (index = vertex id, stride = one row, lane
-//    offset = its slot): no 64-bit address arithmetic per row, and a neighbour slot past the end
-//    of the row carries index -1, which the descriptor's range check (index >= n) turns into a
-//    zero row without a branch or a memory request;
+//  * rows move branch-free: a neighbour slot past the end of the row (or a done neighbour) reads
+//    the all-zero row n of the visited buffers (BitparSolver allocates n + 2 rows; levels()
+//    clears rows n and n + 1 for the word count at hand) and an idle lane stores to the scratch
+//    row n + 1. With MSBFS_SBUF (off by default) the rows move with STRUCTURED buffer loads /
+//    stores (index = vertex id, stride = one row, lane offset = its slot: no 64-bit address
+//    arithmetic). Measured on gfx950 (tools/ubench/sbuf_check.hip): such a descriptor applies
+//    NO index range check (index == num_records read the row's data), so out-of-range indices
+//    are never issued either way;
 //  * a step's column ids are broadcast inside the lane group with ds_swizzle (constant pattern,
 //    all CS issued before the first use) instead of one ds_bpermute + wait + branch per row;
 //  * the new lists (next active, next wide, new frontier) go through WAVE-private LDS queues with
@@ -37,13 +41,6 @@ __device__ void sbuf_store_b128(bu4 v, __amdgpu_buffer_rsrc_t rsrc, int vindex, 
 __device__ void sbuf_store_b64(bu2 v, __amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset,
                                int soffset, int aux) __asm("llvm.amdgcn.struct.ptr.buffer.store.v2i32");
 
-// Descriptor of a visited buffer: rows of W words, n rows (index >= n reads as zero). The
-// stride field holds 14 bits: rows up to 16 words (128 B).
-template <int W>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint64_t* base, int64_t n) {
-  static_assert(W * 8 < 16384, "descriptor stride");
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)(W * 8), (int)n, 0x00020000);
-}
 // row slice (VW words) of index u at byte offset voff within the row
 template <int VW>
 __device__ __forceinline__ V<VW> ld_row(__amdgpu_buffer_rsrc_t rs, int32_t u, int voff) {
@@ -74,6 +71,46 @@ __device__ __forceinline__ void st_row(__amdgpu_buffer_rsrc_t rs, int32_t u, int
     x.y = (uint32_t)(r.w[0] >> 32);
     sbuf_store_b64(x, rs, u, voff, 0, 0);
   }
+}
+
+#ifndef MSBFS_SBUF
+#define MSBFS_SBUF 0
+#endif
+// The rows of one visited buffer: row u's slice of a lane at byte offset voff (u < n + 2)
+template <int W>
+struct RowBuf {
+#if MSBFS_SBUF
+  __amdgpu_buffer_rsrc_t rs;
+#else
+  uint64_t* base;
+#endif
+};
+template <int W>
+__device__ __forceinline__ RowBuf<W> row_buf(const uint64_t* base, int64_t n) {
+#if MSBFS_SBUF
+  static_assert(W * 8 < 16384, "descriptor stride");
+  return RowBuf<W>{__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)(W * 8), (int)(n + 2),
+                                                     0x00020000)};
+#else
+  (void)n;
+  return RowBuf<W>{(uint64_t*)base};
+#endif
+}
+template <int W, int VW>
+__device__ __forceinline__ V<VW> ld_row(const RowBuf<W>& b, int32_t u, int voff) {
+#if MSBFS_SBUF
+  return ld_row<VW>(b.rs, u, voff);
+#else
+  return ldv<VW>(b.base + (int64_t)u * W + voff / 8);
+#endif
+}
+template <int W, int VW>
+__device__ __forceinline__ void st_row(const RowBuf<W>& b, int32_t u, int voff, const V<VW>& r) {
+#if MSBFS_SBUF
+  st_row<VW>(b.rs, u, voff, r);
+#else
+  stv<VW>(b.base + (int64_t)u * W + voff / 8, r);
+#endif
 }
 
 // lanes below this one among the set bits of a wave mask (v_mbcnt)
@@ -162,8 +199,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
   int32_t* qf = qa + QA;
   int32_t* qw = qf + QF;
   uint32_t na = 0, nf = 0, nw = 0;  // (wave-uniform)
-  const __amdgpu_buffer_rsrc_t rR = row_rsrc<W>(R, n), rO = row_rsrc<W>(Wb, n);
+  const RowBuf<W> rR = row_buf<W>(R, n), rO = row_buf<W>(Wb, n);
   const int voff = slot * VW * 8;
+  const int32_t zrow = (int32_t)n, srow = (int32_t)n + 1;  // all-zero row, scratch row
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
@@ -182,7 +220,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
   // row / offsets / column entry 0) with the result selected after: a load under a branch made
   // the compiler wait for it at the branch's end (s_waitcnt vmcnt(0) across basic blocks), which
   // undid the pipeline (round-3 k_bu_narrow waited for its prefetched offsets on the spot).
-  V<VW> r1 = ld_row<VW>(rR, v1, voff);  // (v1 = -1: zeros)
+  V<VW> r1 = ld_row<W, VW>(rR, v1 >= 0 ? v1 : zrow, voff);
   int64_t b1 = rowptr[v1 >= 0 ? v1 : 0], e1 = rowptr[(v1 >= 0 ? v1 : 0) + 1];
   if (v1 < 0) e1 = b1;
   constexpr int F1 = C1 > 0 ? C1 : C;  // neighbours of the first step
@@ -228,7 +266,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
     }
     // prefetch: row / offsets of the next tile, list entry of the one after
     v1 = idx + stride < nact ? v2 : -1;
-    r1 = ld_row<VW>(rR, v1, voff);
+    r1 = ld_row<W, VW>(rR, v1 >= 0 ? v1 : zrow, voff);
     b1 = rowptr[v1 >= 0 ? v1 : 0];
     e1 = rowptr[(v1 >= 0 ? v1 : 0) + 1];
     {
@@ -263,11 +301,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
 #pragma unroll
             for (int j = 0; j < VW; ++j) acc.w[j] = am.w[j];
         }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) u0[q] = u0[q] >= 0 ? u0[q] : zrow;
         int32_t uc[F1];
         bcast_ids<G, Q, F1>(u0, uc, std::make_integer_sequence<int, F1>{});
         V<VW> x[F1];
 #pragma unroll
-        for (int c = 0; c < F1; ++c) x[c] = ld_row<VW>(rR, uc[c], voff);
+        for (int c = 0; c < F1; ++c) x[c] = ld_row<W, VW>(rR, uc[c], voff);
         // (the next tile's first-step ids behind the rows: waiting for the rows leaves them in
         // flight; their offsets were loaded at the top of this tile)
         if (v1 < 0) e1 = b1;
@@ -303,11 +343,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
 #pragma unroll
             for (int j = 0; j < VW; ++j) acc.w[j] |= am.w[j];
         }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) u[q] = u[q] >= 0 ? u[q] : zrow;
         int32_t uc[C];
         bcast_ids<G, Q, C>(u, uc, std::make_integer_sequence<int, C>{});
         V<VW> x[C];
 #pragma unroll
-        for (int c = 0; c < C; ++c) x[c] = ld_row<VW>(rR, uc[c], voff);
+        for (int c = 0; c < C; ++c) x[c] = ld_row<W, VW>(rR, uc[c], voff);
         bool cov = true;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
@@ -334,12 +376,12 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
     const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
     const bool g_new = (bn >> (sub * G)) & L::GBITS;
     const bool g_nf = (bf >> (sub * G)) & L::GBITS;
-    {  // also when nothing is open: Wb may hold the previous batch's rows (invalid lanes: index -1)
+    {  // also when nothing is open: Wb may hold the previous batch's rows (idle lanes: scratch row)
       // (skip: a vertex done now is never read again, see above)
       V<VW> nv;
 #pragma unroll
       for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nwv.w[j];
-      st_row<VW>(rO, valid && (g_nf || !skip) ? v : -1, voff, nv);
+      st_row<W, VW>(rO, valid && (g_nf || !skip) ? v : srow, voff, nv);
     }
     bc.add(nwv);  // (zero for invalid lanes)
     if (++nadd == (1 << BitCounter<VW>::D) - 1) {

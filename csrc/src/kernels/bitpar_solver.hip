@@ -99,7 +99,8 @@ BitparSolver::BitparSolver(const DeviceGraph& g, int max_groups)
     }
   }
   maxW_ = w;
-  const size_t vb = (size_t)n * maxW_ * sizeof(uint64_t);
+  // (+ 2 rows: the all-zero row n and the scratch row n + 1 of k_bu_full's branch-free gathers)
+  const size_t vb = (size_t)(n + 2) * maxW_ * sizeof(uint64_t);
   for (int i = 0; i < 2; ++i) {
     vis_[i].alloc(vb);
     acc_[i].alloc(vb);
@@ -233,6 +234,10 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
 template <int W, bool COUNT>
 void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
   const Small sm = small();
+  // rows n (all-zero) and n + 1 (scratch) of this word count (see bitpar/pull_full.hpp)
+  for (int i = 0; i < 2; ++i)
+    MSBFS_HIP_CHECK(hipMemsetAsync(vis_[i].as<uint64_t>() + (size_t)std::max<int64_t>(g_.n, 1) * W,
+                                   0, 2 * W * sizeof(uint64_t), s));
   static const bool trace = getenv("MSBFS_TRACE") != nullptr;
   auto tl = std::chrono::steady_clock::now();
   HostCtr c{};
