@@ -473,7 +473,7 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
 // covers every alive group (probe instead of its row); every vertex this pass finishes is done,
 // so with skip it writes no row at all.
 template <int W>
-__global__ __launch_bounds__(kBlock, 8) void k_bu_first(
+__global__ __launch_bounds__(kBlock, W >= 16 ? 8 : 6) void k_bu_first(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF, const int32_t* first,

@@ -167,8 +167,13 @@ __device__ __forceinline__ bool done_in(const uint32_t* snap, int32_t u) {
 // CS neighbours per step; C1 > 0: a first step of only C1 rows (late levels are mostly covered by
 // the first neighbour, rows sorted hubs first). nact_dev: list length on the device (device-driven
 // levels). gate: closed levels of a device-driven batch are no-ops. dsnap / skip: see above.
-template <int W, int CS = 8, int C1 = 0>
-__global__ __launch_bounds__(kBlock, 4) void k_bu_full(
+// Few words (W <= 4: phase C of the hybrid mode at 8 ranks, RMAT-30's 32-group passes): 4-row
+// steps; up to 2 words also a 96-VGPR bound, five waves per SIMD (with 8-row steps: 110-128 VGPRs,
+// four waves per SIMD, and the pull is latency-bound there).
+template <int W>
+constexpr int full_cs() { return W <= 4 ? 4 : 8; }
+template <int W, int CS = full_cs<W>(), int C1 = 0>
+__global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, int64_t n, const uint64_t* alive, const uint64_t* gmask,
     uint32_t* done, int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* actw2,
@@ -206,7 +211,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long eu = 0, ef = 0, ev = 0;
-  BitCounter<VW> bc;
+  // (5 slices for few words: one spill every 31 tiles, 4 fewer VGPRs)
+  BitCounter<VW, W <= 4 ? 5 : 6> bc;
   bc.zero();
   int nadd = 0;
   // software pipeline (as k_bu_narrow): list entry two tiles ahead, own row / offsets one tile
@@ -384,7 +390,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_bu_full(
       st_row<W, VW>(rO, valid && (g_nf || !skip) ? v : srow, voff, nv);
     }
     bc.add(nwv);  // (zero for invalid lanes)
-    if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+    if (++nadd == (1 << decltype(bc)::D) - 1) {
       bc.template spill_strided<CR>(cnt, slot);
       nadd = 0;
     }

@@ -293,7 +293,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gl;
         if (tun_.full)
-          k_bu_full<W, 8, 1><<<gn, kBlock, 0, s>>>(
+          k_bu_full<W, full_cs<W>(), 1><<<gn, kBlock, 0, s>>>(
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
               done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
@@ -308,7 +308,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gn;
       } else if (FUSE && !filt && tun_.full) {
-        auto kf = short1 ? k_bu_full<W, 8, 1> : k_bu_full<W, 8, 0>;
+        auto kf = short1 ? k_bu_full<W, full_cs<W>(), 1> : k_bu_full<W, full_cs<W>(), 0>;
         kf<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive,
                                  sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                  fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
@@ -459,7 +459,7 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
                     const uint64_t* alive, int32_t* fl_out, Ctr* out, uint32_t* slab,
                     const uint32_t* len, const BuGate& gate, int p) {
     if (full)
-      k_bu_full<W, 8, 1><<<grid, kBlock, 0, s>>>(
+      k_bu_full<W, full_cs<W>(), 1><<<grid, kBlock, 0, s>>>(
           list, 0, g_.rowptr, g_.col, R, O, g_.n, alive, sm.gmask, done_.as<uint32_t>(),
           act_[p ^ 1].as<int32_t>(), fl_out, out, anyvis_.as<uint32_t>(),
           actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate, dsnap, dsnap ? 1 : 0);
