@@ -50,6 +50,45 @@ def test_word_split_and_exchange_layout(K, world):
             assert np.array_equal(rows, want)
 
 
+@pytest.mark.parametrize("K,world,chunks", [(1024, 8, 4), (700, 3, 5), (64, 4, 2), (300, 1, 3)])
+def test_chunked_exchange_layout(K, world, chunks):
+    """The overlapped exchange's pieces (chunk_views: piece c carries every rank's own-vertex
+    range c, any monotone split, some pieces empty) deliver exactly the dense all-to-all: every
+    word lands where k_hybrid_setup reads it."""
+    import torch
+    H = _H()
+    wbeg = H.word_split(K, world)
+    wt = int(wbeg[-1])
+    rng = np.random.default_rng(K + world + chunks)
+    n, n_eff = 301, 290
+    vis = rng.integers(0, 2**62, size=(n, 16), dtype=np.uint64)
+    pc = [H.part_count(n_eff, r, world) for r in range(world)]
+    # per-rank bounds: uneven, an empty piece in the middle where possible
+    bounds = np.zeros((world, chunks + 1), dtype=np.int64)
+    for r in range(world):
+        cuts = np.sort(rng.integers(0, pc[r] + 1, size=chunks - 1))
+        if chunks > 2:
+            cuts[1] = cuts[0]
+        bounds[r, 1:-1] = cuts
+        bounds[r, -1] = pc[r]
+    sends = [torch.from_numpy(H.pack_words_np(vis, r, world, n_eff, wbeg).view(np.int64))
+             for r in range(world)]
+    want = H.all_to_all_np([x.numpy().view(np.uint64) for x in sends], n_eff, wbeg)
+    recvs = [torch.full((max(1, len(want[j])),), -1, dtype=torch.int64) for j in range(world)]
+    for c in range(chunks):
+        views = [H.chunk_views(sends[r], recvs[r], pc[r], wbeg, r, pc, bounds, c)
+                 for r in range(world)]
+        for j in range(world):  # emulated all_to_all of piece c
+            for r in range(world):
+                ins_r, _ = views[r]
+                _, outs_j = views[j]
+                assert outs_j[r].numel() == ins_r[j].numel()
+                outs_j[r].copy_(ins_r[j])
+    for j in range(world):
+        got = recvs[j].numpy().view(np.uint64)[:len(want[j])]
+        assert np.array_equal(got, want[j]), (j, wt)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
