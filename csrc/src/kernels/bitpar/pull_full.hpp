@@ -11,9 +11,9 @@
 //    clears rows n and n + 1 for the word count at hand) and an idle lane stores to the scratch
 //    row n + 1. With MSBFS_SBUF (off by default) the rows move with STRUCTURED buffer loads /
 //    stores (index = vertex id, stride = one row, lane offset = its slot: no 64-bit address
-//    arithmetic). Measured on gfx950 (tools/ubench/sbuf_check.hip): such a descriptor applies
-//    NO index range check (index == num_records read the row's data), so out-of-range indices
-//    are never issued either way;
+//    arithmetic). Measured on gfx950 (tools/ubench/sbuf_check.hip, round 4): such a descriptor
+//    applies no index range check, and index * stride stops at 4 GiB (every row >= 2^25 of a
+//    128-byte-row buffer read row 2^25 - 1), so MSBFS_SBUF stays off (8.6-GB RMAT-26 buffers);
 //  * a step's column ids are broadcast inside the lane group with ds_swizzle (constant pattern,
 //    all CS issued before the first use) instead of one ds_bpermute + wait + branch per row;
 //  * the new lists (next active, next wide, new frontier) go through WAVE-private LDS queues with
@@ -164,6 +164,30 @@ __device__ __forceinline__ bool done_in(const uint32_t* snap, int32_t u) {
   return u >= 0 && ((snap[u >> 5] >> (u & 31)) & 1u);
 }
 
+// The end-of-kernel flush of every wave's queue: the block's waves publish their counts, one
+// lane takes the block's run with one atomic, each wave writes its items at its offset.
+// Block-uniform (every thread calls it); wbase: kWaves + 1 LDS words.
+__device__ __forceinline__ void wq_flush_block(int32_t* q, uint32_t& n, int32_t* out,
+                                               uint32_t* gcnt, uint32_t* wbase) {
+  const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  __syncthreads();
+  if (lane_id() == 0) wbase[wv] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < nwv; ++w) {
+      const uint32_t c = wbase[w];
+      wbase[w] = t;
+      t += c;
+    }
+    wbase[nwv] = t ? atomicAdd(gcnt, t) : 0u;
+  }
+  __syncthreads();
+  const uint32_t base = wbase[nwv] + wbase[wv];
+  for (uint32_t i = lane_id(); i < n; i += 64) out[base + i] = q[i];
+  n = 0;
+}
+
 // CS neighbours per step; C1 > 0: a first step of only C1 rows (late levels are mostly covered by
 // the first neighbour, rows sorted hubs first). nact_dev: list length on the device (device-driven
 // levels). gate: closed levels of a device-driven batch are no-ops. dsnap / skip: see above.
@@ -188,12 +212,16 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   static_assert(G * Q == C, "a step is whole lane groups");
   static_assert(C1 == 0 || C1 <= C, "short first step");
   constexpr bool kCombine = G <= 4;
-  // per-wave queues: next narrow active list, new frontier, next wide list
-  // (a flush when another tile's pushes might not fit: every VPW tiles at most)
-  constexpr int QA = VPW >= 64 ? 512 : 448, QF = QA, QW = 2 * VPW > 64 ? 2 * VPW : 64;
+  // per-wave queues: next narrow active list, new frontier, next wide list. A flush (one
+  // same-address atomic, ~12 ns each at the memory side, serialised per counter) comes when
+  // another tile's pushes might not fit; 1024-item queues keep them at about the round-3 block
+  // queues' count (448-item ones made level 3 pay ~170K of them) and fill the LDS of four
+  // blocks per CU (the VGPR bound) exactly (768 for up to 2 words: five blocks per CU).
+  constexpr int QA = W <= 2 ? 768 : 1024, QF = QA, QW = 2 * VPW > 128 ? 2 * VPW : 128;
   static_assert(QW >= 2 * VPW, "a wide push always fits after a flush");
   __shared__ int32_t qmem[kWaves][QA + QF + QW];
   __shared__ unsigned long long scratch[kWaves];
+  __shared__ uint32_t wbase[kWaves + 1];
   constexpr int CR = 65;  // bank-skewed counter rows (BitCounter::spill_strided)
   __shared__ uint32_t cnt[CR * W];
   for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
@@ -413,9 +441,11 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
     if (nw + VPW > QW) wq_flush(qw, nw, actw2, &ctr->actw2.v);
     if (nf + VPW > QF) wq_flush(qf, nf, fl2, &ctr->fl2.v);
   }
-  wq_flush(qa, na, act2, &ctr->act2.v);
-  wq_flush(qw, nw, actw2, &ctr->actw2.v);
-  wq_flush(qf, nf, fl2, &ctr->fl2.v);
+  // the rest of every wave's queues: one atomic per block and list (a block barrier is free at
+  // the end; per-wave atomics here were 3 x 8192 on three addresses)
+  wq_flush_block(qa, na, act2, &ctr->act2.v, wbase);
+  wq_flush_block(qw, nw, actw2, &ctr->actw2.v, wbase);
+  wq_flush_block(qf, nf, fl2, &ctr->fl2.v, wbase);
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);

@@ -158,6 +158,9 @@ class BitparSolver final : public Solver {
     bool keep_rows = false;             // every row written (hybrid phase A packs them)
     bool skip_pending = false;
     const uint64_t* skip_alive = nullptr;
+    // a level skipped rows: every later pull level of the batch probes dsnap_ (re-snapshotted
+    // at the start of the first pull level after each skipping level)
+    bool skipped_any = false, resnap = false;
   };
   struct Small {
     unsigned long long* F;
@@ -333,8 +336,9 @@ class BitparSolver final : public Solver {
   bool tiles_ok_ = true;  // false once the tiles did not fit
   DevBuf fbm_tile_, lcnt_, zrow_;  // frontier bitmap of a tiled level, list counter, zero row
   DevBuf dsnap_;                   // done bitmap as of a dskip level's start
-  // dskip for the next pull level: snapshot of the done bitmap (nullptr: off for this level)
-  const uint32_t* done_snapshot(const Loop& S, bool unfiltered, hipStream_t s);
+  // dskip: the done-bitmap snapshot a pull level probes (nullptr: no probes); skip_now: this
+  // level skips the rows of the vertices it finishes
+  const uint32_t* done_probe(Loop& S, bool skip_now, hipStream_t s);
   template <int W>
   void fix_done_rows(Loop& S, hipStream_t s);
   int num_cus_ = 0;

@@ -101,14 +101,23 @@ void BitparSolver::prepare(hipStream_t s) {
   (void)ne;
 }
 
-// dskip (see pull_full.hpp): the done bitmap as of this level's start, for the unfiltered pull
-// levels (a filtered level never follows one in a batch: ev only grows; not in hybrid phase A,
-// which packs the rows; not in the edge-counting pass)
-const uint32_t* BitparSolver::done_snapshot(const Loop& S, bool unfiltered, hipStream_t s) {
-  if (!tun_.dskip || !tun_.full || S.keep_rows || !unfiltered) return nullptr;
+// dskip (see pull_full.hpp). Rows are skipped only by the lean first-row pass (and its overflow
+// pull): there ~98 % of the active vertices finish (RMAT-26 level 4: 24.4M rows not written).
+// Measured (round 4, RMAT-26 / 1024 groups): probing on every unfiltered level cost level 3
+// +0.55 ms (a dependent 4-byte load per step for vertices whose neighbours are never done) for
+// -0.25 ms at level 4. A vertex done at a skipping level L keeps a stale row, so every later pull
+// level of the batch probes a snapshot of the done bitmap taken at the start of level L + 1
+// (one copy: vertices done after it wrote their rows); level L itself probes the snapshot of its
+// own start (its first neighbours: a done hub covers the vertex without a row gather).
+const uint32_t* BitparSolver::done_probe(Loop& S, bool skip_now, hipStream_t s) {
+  if (!skip_now && !S.skipped_any) return nullptr;
   const size_t b = (size_t)((g_.n + 31) / 32) * sizeof(uint32_t);
-  dsnap_.ensure(std::max<size_t>(b, 4));
-  MSBFS_HIP_CHECK(hipMemcpyAsync(dsnap_.p, done_.p, b, hipMemcpyDeviceToDevice, s));
+  if (skip_now || S.resnap) {
+    dsnap_.ensure(std::max<size_t>(b, 4));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(dsnap_.p, done_.p, b, hipMemcpyDeviceToDevice, s));
+  }
+  S.resnap = skip_now;
+  S.skipped_any |= skip_now;
   return dsnap_.as<uint32_t>();
 }
 
@@ -196,12 +205,15 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   // has the LDS to itself, 128 KB (ids < 1M)
   const bool hub_lds = filter_from == 0 && n > (int64_t)kHubW * 32 * 4;
   const bool hub_big = n > (int64_t)kHubBig * 32 * 4;
-  // dskip: probes of done neighbours (and no rows for finishing vertices) on the unfiltered
-  // levels after the first pull level, all of whose kernels probe (k_bu_full, k_bu_first, the
-  // hub chunks); the per-vertex pulls of tun_.full = 0 do not
-  const uint32_t* dsnap =
-      (!COUNT && !tiled) ? done_snapshot(S, filter_from == INT32_MAX && !lazy_first, s) : nullptr;
-  S.skip_pending = dsnap != nullptr;
+  // dskip (see done_probe): the lean pass skips the rows of the vertices it finishes; a filtered
+  // level never follows it in a batch (ev only grows), and the unfiltered kernels all probe
+  // (k_bu_full, k_bu_first, the hub chunks; not the per-vertex pulls of tun_.full = 0)
+  const bool lean_now = tun_.lean && !S.lean_off && FUSE && filter_from == INT32_MAX &&
+                        !tiled && !pfx && S.bu_levels >= tun_.lean_level &&
+                        S.nact >= tun_.lean_min;
+  const bool skip_now = lean_now && !COUNT && tun_.dskip && tun_.full && !S.keep_rows;
+  const uint32_t* dsnap = (!COUNT && tun_.full) ? done_probe(S, skip_now, s) : nullptr;
+  S.skip_pending = skip_now;
   S.skip_alive = alive;
   // counting fused into the traversal kernels (the edge-count pass keeps k_count_frontier)
   constexpr bool FUSE = !COUNT;
@@ -289,7 +301,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
             act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
             done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
             ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
-            dsnap ? 1 : 0);
+            skip_now ? 1 : 0);
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gl;
         if (tun_.full)
@@ -297,7 +309,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
               done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
-              slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{}, dsnap, dsnap ? 1 : 0);
+              slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{}, dsnap, skip_now ? 1 : 0);
         else
           k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
@@ -313,7 +325,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                                  sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                  fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                  anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
-                                 slabF<W>(rows), nullptr, BuGate{}, dsnap, dsnap ? 1 : 0);
+                                 slabF<W>(rows), nullptr, BuGate{}, dsnap, 0);
         rows += gn;
       } else {
         auto kn = FUSE ? (filt ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, true>
@@ -447,14 +459,9 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
   trace::Range range_batch("bitpar L%u-%u BU batch", level0 + 1, level0 + K);
   auto kn = k_bu_narrow<W, false, kBlock, 0, true, false, false, 8, 1>;
   const bool full = tun_.full != 0;
-  // dskip: every level of the batch snapshots the done bitmap at its start (a copy on the stream,
-  // also for the levels whose gate closes)
-  const bool dsk = full && tun_.dskip && !S.keep_rows;
-  const uint32_t* dsnap = nullptr;
-  if (dsk) {
-    dsnap_.ensure(std::max<size_t>((size_t)((g_.n + 31) / 32) * sizeof(uint32_t), 4));
-    dsnap = dsnap_.as<uint32_t>();
-  }
+  // dskip: after a skipping level the batch's levels probe the snapshot (taken once, before the
+  // first of them); they skip nothing themselves
+  const uint32_t* dsnap = full ? done_probe(S, false, s) : nullptr;
   auto launch = [&](int grid, const int32_t* list, const uint64_t* R, uint64_t* O,
                     const uint64_t* alive, int32_t* fl_out, Ctr* out, uint32_t* slab,
                     const uint32_t* len, const BuGate& gate, int p) {
@@ -462,7 +469,7 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
       k_bu_full<W, full_cs<W>(), 1><<<grid, kBlock, 0, s>>>(
           list, 0, g_.rowptr, g_.col, R, O, g_.n, alive, sm.gmask, done_.as<uint32_t>(),
           act_[p ^ 1].as<int32_t>(), fl_out, out, anyvis_.as<uint32_t>(),
-          actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate, dsnap, dsnap ? 1 : 0);
+          actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate, dsnap, 0);
     else
       kn<<<grid, kBlock, 0, s>>>(list, 0, g_.rowptr, g_.col, R, O, alive, sm.gmask,
                                  done_.as<uint32_t>(), act_[p ^ 1].as<int32_t>(), fl_out, out,
@@ -476,9 +483,6 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
     uint64_t* O = vis_[S.cur ^ p ^ 1].as<uint64_t>();
     int32_t* fl_out = fl_[S.fc ^ p ^ 1].as<int32_t>();
     const uint64_t* alive = aslot + 16 * i;
-    if (dsnap)
-      MSBFS_HIP_CHECK(hipMemcpyAsync(dsnap_.p, done_.p, (size_t)((g_.n + 31) / 32) * 4,
-                                     hipMemcpyDeviceToDevice, s));
     launch(gn, act_[p].as<int32_t>(), R, O, alive, fl_out, slots + i + 1, slabF<W>(0),
            &slots[i].act2.v, gate, p);
     if (gw)
@@ -536,8 +540,7 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
   S.osnap_next = false;
   // (the last real level's alive mask stays in bctr_ until the next batch: a push level right
   // after restores the skipped rows of its frontier first, see levels())
-  S.skip_pending = dsnap && real > 0;
-  S.skip_alive = aslot + 16 * std::max(real - 1, 0);
+  if (real > 0) S.skip_pending = false;  // (a skipping level's frontier: restored only if next)
   // the next batch: twice as long while the frontier lives, else this tail's length + 1
   bu_next_ = real == K ? std::min(2 * K, kBatch) : real + 1;
 }
