@@ -205,16 +205,6 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   // has the LDS to itself, 128 KB (ids < 1M)
   const bool hub_lds = filter_from == 0 && n > (int64_t)kHubW * 32 * 4;
   const bool hub_big = n > (int64_t)kHubBig * 32 * 4;
-  // dskip (see done_probe): the lean pass skips the rows of the vertices it finishes; a filtered
-  // level never follows it in a batch (ev only grows), and the unfiltered kernels all probe
-  // (k_bu_full, k_bu_first, the hub chunks; not the per-vertex pulls of tun_.full = 0)
-  const bool lean_now = tun_.lean && !S.lean_off && FUSE && filter_from == INT32_MAX &&
-                        !tiled && !pfx && S.bu_levels >= tun_.lean_level &&
-                        S.nact >= tun_.lean_min;
-  const bool skip_now = lean_now && !COUNT && tun_.dskip && tun_.full && !S.keep_rows;
-  const uint32_t* dsnap = (!COUNT && tun_.full) ? done_probe(S, skip_now, s) : nullptr;
-  S.skip_pending = skip_now;
-  S.skip_alive = alive;
   // counting fused into the traversal kernels (the edge-count pass keeps k_count_frontier)
   constexpr bool FUSE = !COUNT;
   // prefix pull + tail push on the first bottom-up level (see k_push_tail): the pulls stop at
@@ -225,6 +215,16 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   // sparse row codes for the first bottom-up level after level 1 (see k_build_codes). With
   // the prefix pull only ids < H and the tail pushers' own codes are ever read: the codes of
   // [code_from, H) plus those of the frontier vertices >= H (not 4 bytes for every id).
+  // dskip (see done_probe): the lean pass skips the rows of the vertices it finishes; a filtered
+  // level never follows it in a batch (ev only grows), and the unfiltered kernels all probe
+  // (k_bu_full, k_bu_first, the hub chunks; not the per-vertex pulls of tun_.full = 0)
+  const bool lean_now = tun_.lean && !S.lean_off && FUSE && filter_from == INT32_MAX &&
+                        !tiled && !pfx && S.bu_levels >= tun_.lean_level &&
+                        S.nact >= tun_.lean_min;
+  const bool skip_now = lean_now && !COUNT && tun_.dskip && tun_.full && !S.keep_rows;
+  const uint32_t* dsnap = (!COUNT && tun_.full) ? done_probe(S, skip_now, s) : nullptr;
+  S.skip_pending = skip_now;
+  S.skip_alive = alive;
   int32_t code_from = kNoCodes;
   const uint32_t* codes = nullptr;
   if (first_bu && S.level == 2 && tun_.codes && W >= 8 && S.ef0 > 0 && n <= INT32_MAX) {
