@@ -534,7 +534,7 @@ __global__ __launch_bounds__(kBlock, W >= 16 ? 8 : 6) void k_bu_first(
     }
     bc.add(nw);
     if (++nadd == (1 << BitCounter<VW>::D) - 1) {
-      bc.template spill_strided<CR>(cnt, slot);
+      bc.template spill_strided32<CR>(cnt, slot);
       nadd = 0;
     }
     bool anynew = false;
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(kBlock, W >= 16 ? 8 : 6) void k_bu_first(
   q_flush(qf, fl2, &ctr->fl2.v, 0, true);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
-  bc.template spill_strided<CR>(cnt, slot);
+  bc.template spill_strided32<CR>(cnt, slot);
   __syncthreads();
   uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
   for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];

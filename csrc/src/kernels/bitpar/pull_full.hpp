@@ -239,8 +239,11 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long eu = 0, ef = 0, ev = 0;
-  // (5 slices for few words: one spill every 31 tiles, 4 fewer VGPRs)
-  BitCounter<VW, W <= 4 ? 5 : 6> bc;
+  // Carry-save group counters: 7 slices (a spill every 127 tiles) at 16 words, spilled on
+  // 32-bit halves (~12 VALU per set counter bit instead of ~28: level 3 spills find most
+  // counter bits set, ~50 VALU per tile with 6 slices and 64-bit spills); 5 slices for few
+  // words (one spill every 31 tiles, the 96-VGPR bound)
+  BitCounter<VW, W <= 4 ? 5 : (W >= 16 ? 7 : 6)> bc;
   bc.zero();
   int nadd = 0;
   // software pipeline (as k_bu_narrow): list entry two tiles ahead, own row / offsets one tile
@@ -341,7 +344,13 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
         bcast_ids<G, Q, F1>(u0, uc, std::make_integer_sequence<int, F1>{});
         V<VW> x[F1];
 #pragma unroll
-        for (int c = 0; c < F1; ++c) x[c] = ld_row<W, VW>(rR, uc[c], voff);
+        for (int c = 0; c < F1; ++c) {
+          // (only the slots some vertex of the wave has: degree-sorted lists make a wave's
+          // degrees alike, and every issued slot costs the address unit a full instruction;
+          // gathering all F1 slots ran level 3 at 76 % TA busy)
+          x[c] = vzero<VW>();
+          if (__ballot(beg + c < end)) x[c] = ld_row<W, VW>(rR, uc[c], voff);
+        }
         // (the next tile's first-step ids behind the rows: waiting for the rows leaves them in
         // flight; their offsets were loaded at the top of this tile)
         if (v1 < 0) e1 = b1;
@@ -383,7 +392,10 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
         bcast_ids<G, Q, C>(u, uc, std::make_integer_sequence<int, C>{});
         V<VW> x[C];
 #pragma unroll
-        for (int c = 0; c < C; ++c) x[c] = ld_row<W, VW>(rR, uc[c], voff);
+        for (int c = 0; c < C; ++c) {
+          x[c] = vzero<VW>();
+          if (__ballot(e + c < end)) x[c] = ld_row<W, VW>(rR, uc[c], voff);
+        }
         bool cov = true;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
@@ -419,7 +431,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
     }
     bc.add(nwv);  // (zero for invalid lanes)
     if (++nadd == (1 << decltype(bc)::D) - 1) {
-      bc.template spill_strided<CR>(cnt, slot);
+      bc.template spill_strided32<CR>(cnt, slot);
       nadd = 0;
     }
     const bool leader = valid && slot == 0;
@@ -449,7 +461,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
-  bc.template spill_strided<CR>(cnt, slot);
+  bc.template spill_strided32<CR>(cnt, slot);
   __syncthreads();
   uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
   for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
