@@ -189,8 +189,10 @@ void BitparSolver::phase_a_impl(int64_t K, const int64_t* qoff, const int32_t* q
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   if (chunks > 1) {
-    // ranges the level did not hand out (no tiled level-2 pull): packed now, in order
-    for (int c = S.chunks_done; c < chunks; ++c) {
+    // ranges the level did not hand out (no tiled level-2 pull): packed now, in the tiled
+    // pull's order (last range first; every rank must start its pieces in the same order)
+    for (int k = S.chunks_done; k < chunks; ++k) {
+      const int c = chunks - 1 - k;
       pack(vis_[S.cur].as<uint64_t>(), S.chunk_b[(size_t)c], S.chunk_b[(size_t)c + 1]);
       cb(user, c, S.chunk_b[(size_t)c], S.chunk_b[(size_t)c + 1]);
     }

@@ -156,9 +156,11 @@ void BitparSolver::prepare_hybrid(int part, int nparts, hipStream_t s) {
 }
 
 // Own-vertex ranges of a chunked phase A (device.hpp): from the tile set, split at tile starts
-// into pieces of about equal prefix entries; the first piece holds every big vertex's partial
-// tiles (k_bu_wide_finalize runs after it). Without tiles: an even split (the ranges are then
-// packed after the level).
+// into pieces of about equal tile counts (a tile is ~kTileWeight of entries and vertices; equal
+// prefix entries gave RMAT-26 / 8 parts pieces ready at 1.72, 1.72, 1.99 and 2.89 ms: the
+// low-degree end is vertex-bound); the first piece holds every big vertex's partial tiles
+// (k_bu_wide_finalize runs after it). Without tiles: an even split (the ranges are then packed
+// after the level).
 void BitparSolver::hybrid_chunk_bounds(int part, int nparts, int64_t n_eff, int chunks,
                                        int64_t* b, hipStream_t s) {
   if (chunks < 1) fail("hybrid: chunks must be >= 1");
@@ -172,8 +174,7 @@ void BitparSolver::hybrid_chunk_bounds(int part, int nparts, int64_t n_eff, int 
   b[0] = 0;
   int64_t t = 0;
   for (int c = 1; c < chunks; ++c) {
-    const int64_t target = T->nent * c / chunks;
-    int64_t tc = std::lower_bound(T->te.begin(), T->te.end() - 1, target) - T->te.begin();
+    int64_t tc = T->ntiles * c / chunks;
     if (c == 1) tc = std::max(tc, T->last_partial + 1);
     t = std::max(t, std::min(tc, T->ntiles));
     b[c] = T->ti[(size_t)t];
@@ -212,12 +213,21 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
     MSBFS_HIP_CHECK(hipGetLastError());
     rows += gw;
   };
-  int64_t t0 = 0;
-  for (int c = 0; c < nch; ++c) {
-    int64_t t1 = T->ntiles;
-    if (nch > 1 && c + 1 < nch)  // first tile of the next range
-      t1 = std::lower_bound(T->ti.begin(), T->ti.end() - 1, S.chunk_b[(size_t)c + 1]) -
+  auto tile_at = [&](int c) -> int64_t {  // first tile of range c
+    if (c <= 0) return 0;
+    if (c >= nch) return T->ntiles;
+    return std::lower_bound(T->ti.begin(), T->ti.end() - 1, S.chunk_b[(size_t)c]) -
            T->ti.begin();
+  };
+  // ranges from the last (low-degree end) to the first (hubs): pieces go out in the order
+  // their words are packed and the low-degree ranges hold most own vertices, i.e. most bytes
+  // per tile, so the big pieces overlap the remaining tiles and the exchange still running when
+  // the level ends is the hubs' small piece. RMAT-26, 8 parts, 4 ranges: the first piece was
+  // ready at 1.7 of 3.0 ms and 1.24 of the 1.75 ms exchange (at 300 GB/s) was exposed in
+  // range order. (Every rank hands its pieces out in this same order: the collectives pair up.)
+  for (int k = 0; k < nch; ++k) {
+    const int c = nch - 1 - k;
+    const int64_t t0 = tile_at(c), t1 = tile_at(c + 1);
     if (t1 > t0) {
       k_pfx_tiles<W><<<grid, kTileBlock, 0, s>>>(
           T->tiles.as<PfxTile>() + t0, t1 - t0, T->pent.as<uint32_t>(), S.nparts, g_.rowptr, R,
@@ -232,7 +242,6 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
       S.on_chunk(c);
       ++S.chunks_done;
     }
-    t0 = t1;
   }
   // next active lists (a hybrid phase A stops here: nothing reads them)
   if (S.level < S.stop_level) {

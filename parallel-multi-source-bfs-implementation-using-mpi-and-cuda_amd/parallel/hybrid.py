@@ -445,6 +445,10 @@ def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
             timings[len(timings) - world + j]["phase_c_ms"] = sc["device_ms"]
             timings[len(timings) - world + j]["phase_c_wall_ms"] = (time.perf_counter() - tw) * 1e3
             timings[len(timings) - world + j]["levels_c"] = sc["levels"]
+            # per level of phase C: direction, active (pull) / touched (push) vertices, ms
+            timings[len(timings) - world + j]["levels_c_trace"] = [
+                (t["dir"], t["level"], t["active"], round(t["ms"], 3))
+                for t in solver.level_trace()]
         idx = own_groups(K, wbeg, j)
         F[idx] = reduced[idx] + Fc[:len(idx)]
     return F

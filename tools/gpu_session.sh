@@ -49,6 +49,16 @@ for s in "$@"; do
     hybsim) step hybsim 900 python tools/hybrid_sim.py --scale 26 --ranks 2 4 8 ;;
     hybsim8) step hybsim8 600 python tools/hybrid_sim.py --scale 26 --ranks 8 --no-roundrobin ;;
     profhyb8) prof profhyb 900 python tools/hybrid_sim.py --scale 26 --ranks 8 --no-roundrobin ;;
+    profhc)  # kernel timelines of phase C of ranks 0 and 1 (8 emulated ranks)
+      export TMPDIR=/tmp; rm -rf gpurun_out/profhc
+      step profhc 900 rocprofv3 --kernel-trace --stats -T --output-format csv \
+        -d gpurun_out/profhc -o run -- python tools/hybrid_sim.py --scale 26 --ranks 8 \
+        --no-roundrobin --chunks 4 &&
+      for k in 8 7; do PROF_START=k_hybrid_setup PROF_NTH=$k python tools/prof_summary.py \
+        gpurun_out/profhc > "gpurun_out/profhc_r$((8 - k)).md"; done &&
+      PROF_START=k_init PROF_NTH=8 python tools/prof_summary.py gpurun_out/profhc \
+        > gpurun_out/profhc_a0.md &&
+      rm -f gpurun_out/profhc/run_kernel_trace.csv ;;
     pmchbm) export TMPDIR=/tmp; R="k_bu|k_push|k_td|k_build|k_level"; rm -rf gpurun_out/pmch1 gpurun_out/pmch2 gpurun_out/pmch3
          step pmch1 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmch1 -o run -- python bench.py --steps 1 --warmup 0 --verify 0 &&
          step pmch2 300 rocprofv3 --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmch2 -o run -- python bench.py --steps 1 --warmup 0 --verify 0 &&

@@ -45,9 +45,17 @@ def trace_summary(d):
     print("|---|---|---|")
     for k, (c, ms) in sorted(tot.items(), key=lambda x: -x[1][1])[:25]:
         print(f"| `{k}` | {c} | {ms:.3f} |")
-    # timeline of the last solver run: from the last init kernel on
-    starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]).startswith("k_init")]
-    if starts:
+    # timeline of the last solver run: from the last init kernel on (PROF_START=<kernel>
+    # PROF_NTH=<k>: from the k-th last dispatch of that kernel up to the next one, e.g. one
+    # rank's hybrid phase C of tools/hybrid_sim.py: PROF_START=k_hybrid_setup PROF_NTH=8)
+    marker = os.environ.get("PROF_START", "k_init")
+    nth = int(os.environ.get("PROF_NTH", "1"))
+    starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]).startswith(marker)]
+    if len(starts) >= nth:
+        k = len(starts) - nth
+        end = starts[k + 1] if k + 1 < len(starts) else len(rows)
+        rows = rows[:end]
+        starts = starts[:k + 1]
         run = rows[starts[-1]:]
         t0 = int(run[0]["Start_Timestamp"])
         t1 = max(int(r["End_Timestamp"]) for r in run)
