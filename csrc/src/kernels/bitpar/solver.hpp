@@ -86,6 +86,13 @@ struct Tuning {
   // instead of gathering done neighbours' rows, and the rows of vertices finishing on an
   // unfiltered pull level are not written (a push level right after gets them restored)
   int dskip = 1;
+  // lean pass kernel: 0 = k_bu_first (one tile per wave and iteration), 2 / 4 = k_bu_lean with
+  // that many tiles per wave in flight (bitpar/pull_full.hpp)
+  int first_u = 0;
+  // block size of the tiled first pull (1024: hub bitmap in LDS; 256: global hub probes, five
+  // blocks per CU; see k_pfx_tiles)
+  int tiles_bt = 1024;
+  int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->
   // 12: 13.85 -> 13.32 ms)
@@ -93,7 +100,7 @@ struct Tuning {
   std::string dirs;    // forced per-level directions 'T'/'B' (tests, experiments)
 
   void set(const std::string& key, const std::string& value);
-  void parse(const std::string& spec);  // "k=v,k=v"
+  void parse(const std::string& spec);  // "k=v,k=v" (or ";")
   static const Tuning& process_default();  // defaults + MSBFS_TUNE, read once per process
 };
 

@@ -296,12 +296,23 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
           S.nact >= tun_.lean_min) {
         S.lean_ran = true;
         // lean first pass, then the regular pull over the vertices it could not finish
-        const int gl = grid_for(S.nact, L::TILE, grid);
-        k_bu_first<W><<<gl, kBlock, 0, s>>>(
-            act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
-            done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
-            skip_now ? 1 : 0);
+        int gl;
+        if (tun_.first_u) {
+          gl = grid_for(S.nact, L::TILE * tun_.first_u, grid);
+          auto kl = tun_.first_u == 4 ? k_bu_lean<W, 4> : k_bu_lean<W, 2>;
+          kl<<<gl, kBlock, 0, s>>>(
+              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
+              done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
+              skip_now ? 1 : 0);
+        } else {
+          gl = grid_for(S.nact, L::TILE, grid);
+          k_bu_first<W><<<gl, kBlock, 0, s>>>(
+              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+              done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
+              skip_now ? 1 : 0);
+        }
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gl;
         if (tun_.full)
