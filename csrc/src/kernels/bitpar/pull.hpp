@@ -200,6 +200,104 @@ __global__ __launch_bounds__(kBlock) void k_push_tail(
   }
 }
 
+// 32-bit block sum, one atomic per block
+__device__ __forceinline__ void block_sum_add32(uint32_t val, uint32_t* dst, uint32_t* scratch) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
+  __syncthreads();
+  if (lane_id() == 0) scratch[threadIdx.x >> 6] = val;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += scratch[w];
+    if (t) atomicAdd(dst, t);
+  }
+}
+
+// The tail push AFTER the tiled prefix pull (tuning key push_after; one GPU, no chunked
+// exchange): the pushed bits go straight into the level's output rows O, so the tile epilogue
+// reads no acc row (4.2 GB on RMAT-26 / 1024 groups, every tile vertex) and a push whose bit
+// the prefix pull already set costs a plain load instead of an atomic. The push then does the
+// accounting of what it adds (the epilogue has run): per-group counts of the bits its
+// atomicOr newly set (LDS counters -> this block's slab row), and for a vertex it gave its
+// first new bit of the level, the frontier bit (+ count, degree sum), and for one it gave its
+// first bit at all, the any-visited bit (+ degree sum). A vertex the pushed bits complete is
+// left not done (the next pull finds it covered). Census (tools/tail_push_stats.py, RMAT-26):
+// 179K tail pushers, 40.7M pushed edges, 42.5M code slots, 6.9M distinct targets.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_push_tail_after(
+    const int32_t* fl, int64_t nf, int32_t H, const int64_t* rowptr, const int32_t* col,
+    const uint64_t* R, const uint32_t* code, int32_t code_from, uint64_t* O,
+    const uint32_t* done, uint32_t* fbm, uint32_t* anyvis, Ctr* ctr, uint32_t* slabF) {
+  __shared__ uint32_t cnt[64 * W];
+  __shared__ unsigned long long scratch[kWaves];
+  __shared__ uint32_t scratch32[kWaves];
+  for (int i = threadIdx.x; i < 64 * W; i += kBlock) cnt[i] = 0;
+  __syncthreads();
+  unsigned long long ef = 0, ev = 0;
+  uint32_t nfc = 0;
+  const int lane = lane_id();
+  const int64_t grp = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t ngrp = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t i = grp; i < nf; i += ngrp) {
+    const int32_t u = fl[i];
+    if (u < H) continue;
+    const uint32_t c = (code && u >= code_from) ? code[u] : kDenseCode;
+    if (c == 0) continue;
+    const int64_t b = rowptr[u], e = rowptr[u + 1];
+    for (int64_t k = b + lane; k < e; k += 64) {
+      const int32_t v = col[k];
+      // (a vertex done before this level has no output row written by the pull: skip it; one
+      // done during the level has every alive group already)
+      if (is_done(done, v)) continue;
+      bool added = false;
+      if (c != kDenseCode) {
+        for (int s = 0; s < kCodeSlots; ++s) {
+          const int g = code_g(c, s);
+          if (g < 0) continue;
+          unsigned long long* p = (unsigned long long*)&O[(int64_t)v * W + (g >> 6)];
+          const unsigned long long bit = 1ull << (g & 63);
+          if (*p & bit) continue;  // (set by the pull or an earlier push: bits only get set)
+          if (!(atomicOr(p, bit) & bit)) {
+            atomicAdd(&cnt[g], 1u);
+            added = true;
+          }
+        }
+      } else {
+        for (int j = 0; j < W; ++j) {
+          const uint64_t w = R[(int64_t)u * W + j];
+          if (!w) continue;
+          uint64_t nb = w & ~(uint64_t)atomicOr((unsigned long long*)&O[(int64_t)v * W + j],
+                                                (unsigned long long)w);
+          added |= nb != 0;
+          while (nb) {
+            atomicAdd(&cnt[j * 64 + __ffsll((unsigned long long)nb) - 1], 1u);
+            nb &= nb - 1;
+          }
+        }
+      }
+      if (added) {  // (plain loads first: most targets got new bits from the pull already)
+        const uint32_t m = 1u << (v & 31);
+        const bool in_f = (fbm[v >> 5] & m) != 0, seen = (anyvis[v >> 5] & m) != 0;
+        if (!in_f || !seen) {
+          const unsigned long long dv = (unsigned long long)(rowptr[v + 1] - rowptr[v]);
+          if (!in_f && !(atomicOr(&fbm[v >> 5], m) & m)) {
+            ++nfc;
+            ef += dv;
+          }
+          if (!seen && !(atomicOr(&anyvis[v >> 5], m) & m)) ev += dv;
+        }
+      }
+    }
+  }
+  block_sum_add32(nfc, &ctr->fl2.v, scratch32);
+  block_sum_add(ef, &ctr->ef2.v, scratch);
+  block_sum_add(ev, &ctr->ev2.v, scratch);
+  __syncthreads();
+  uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
+  for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i];
+}
+
 // ---------------------------------------------------------------------------------------------
 // bottom-up, narrow vertices: G lanes per vertex, early exit when every alive group is covered.
 // Each step takes C = 8 neighbours: the group's G lanes load and filter them cooperatively
@@ -877,20 +975,6 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     if (c + cstep < cend) d = desc[c + cstep];  // next descriptor, in flight during the pull
     chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop,
                            lst, code, code_from, wacc[threadIdx.x >> 6], snap, dsnap);
-  }
-}
-
-// 32-bit block sum, one atomic per block
-__device__ __forceinline__ void block_sum_add32(uint32_t val, uint32_t* dst, uint32_t* scratch) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
-  __syncthreads();
-  if (lane_id() == 0) scratch[threadIdx.x >> 6] = val;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += scratch[w];
-    if (t) atomicAdd(dst, t);
   }
 }
 

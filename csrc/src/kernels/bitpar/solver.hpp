@@ -89,9 +89,15 @@ struct Tuning {
   // lean pass kernel: 0 = k_bu_first (one tile per wave and iteration), 2 / 4 = k_bu_lean with
   // that many tiles per wave in flight (bitpar/pull_full.hpp)
   int first_u = 0;
-  // block size of the tiled first pull (1024: hub bitmap in LDS; 256: global hub probes, five
-  // blocks per CU; see k_pfx_tiles)
+  // block size of the tiled first pull (1024: hub bitmap in LDS; 256: global hub probes, four
+  // or five blocks per CU; see k_pfx_tiles). Measured (RMAT-26 / 1024 groups, level 2): 12.5 ms
+  // at 1024, 14.1 ms at 256 x 4, 15.4 ms at 256 x 5 (96 VGPRs, spills): the L2 round trip of
+  // the probes costs more than the extra waves hide
   int tiles_bt = 1024;
+  // tiled first pull level: the tail push after the tiles, into the output rows (one GPU, no
+  // chunked exchange; k_push_tail_after) instead of into acc rows every tile vertex reads
+  // (RMAT-26 / 1024 groups: level 2 12.5 -> 10.95 ms, 20.7-21.3 -> 19.1-19.8 ms per step)
+  int push_after = 1;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->
@@ -162,7 +168,8 @@ class BitparSolver final : public Solver {
     int chunks_done = 0;
     // dskip: the last level skipped the rows of the vertices it finished; a push level next
     // restores those of its frontier (k_fix_done_rows) from the read buffer and this alive mask
-    bool keep_rows = false;             // every row written (hybrid phase A packs them)
+    bool keep_rows = false;
+    bool push_after = false;  // this tiled level's tail push runs after the tiles (k_push_tail_after)             // every row written (hybrid phase A packs them)
     bool skip_pending = false;
     const uint64_t* skip_alive = nullptr;
     // a level skipped rows: every later pull level of the batch probes dsnap_ (re-snapshotted

@@ -146,7 +146,9 @@ __device__ __forceinline__ void tile_mask_or(uint32_t* bm, int32_t v0, uint32_t 
 // bound by the LDS). BT = 256 (tuning key tiles_bt): the hub probes read the global bitmap
 // (56 KB, L2-resident) instead, which leaves the LDS to the waves' accumulator rows: BPC
 // (tuning key tiles_bpc: 4 or 5) 256-thread blocks per CU, i.e. BPC waves per SIMD.
-template <int W, int BT = kTileBlock, int BPC = 1>
+// ACC = false (tuning key push_after): the tail push runs after this kernel and ORs its bits
+// into the output rows itself (k_push_tail_after), so no acc row is read here.
+template <int W, int BT = kTileBlock, int BPC = 1, bool ACC = true>
 __global__ __launch_bounds__(BT, BPC) void k_pfx_tiles(
     const PfxTile* __restrict__ tiles, int64_t ntiles, const uint32_t* __restrict__ pent,
     int nparts, const int64_t* rowptr, const uint64_t* R, uint64_t* O, uint64_t* acc,
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(BT, BPC) void k_pfx_tiles(
             // bits pushed by k_push_tail (no stamps: the level's acc rows are all-zero but
             // the pushed ones, and a tile's rows are one contiguous run; the push skips no done
             // vertex either, so every vertex of the tile reads and clears its row)
-            pa[k] = i < nv ? ldv<VW>(acc + vo) : vzero<VW>();
+            pa[k] = ACC && i < nv ? ldv<VW>(acc + vo) : vzero<VW>();
           }
 #pragma unroll
         for (int k = 0; k < NH; ++k) {
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(BT, BPC) void k_pfx_tiles(
             bool pushed = false;
 #pragma unroll
             for (int j = 0; j < VW; ++j) pushed |= pa[k].w[j] != 0;
-            if (pushed) stv<VW>(acc + (int64_t)v * W + slot * VW, vzero<VW>());
+            if (ACC && pushed) stv<VW>(acc + (int64_t)v * W + slot * VW, vzero<VW>());
           }
           V<VW> nw, nvr;
           bool anynew = false, notfull = false, rnz = false;

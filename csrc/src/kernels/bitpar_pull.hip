@@ -245,7 +245,9 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     }
   }
   const int32_t* plen = pfx ? prefix_lens(kPfxH, s) : nullptr;
-  if (pfx) {
+  // (see k_push_tail_after; needs the whole level in one tiles launch and vertex part 0 of 1)
+  S.push_after = pfx && tiled && tun_.push_after && S.nparts == 1 && !S.on_chunk;
+  if (pfx && !S.push_after) {
     ++epoch_;
     k_push_tail<W><<<grid_for(S.nf * 64, kBlock, 8192), kBlock, 0, s>>>(
         fl_[S.fc].as<int32_t>(), S.nf, kPfxH, g_.rowptr, g_.col, R, codes, code_from,
@@ -255,6 +257,17 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   }
   if (tiled) {
     rows = tiles_pull<W>(S, s, R, O, snap, codes, code_from, rows);
+    if (S.push_after) {
+      const int gp = grid_for(S.nf * 64, kBlock, kMaxGrid);
+      if (rows + gp > 3 * kMaxGrid) fail("tail push: counter slab rows exhausted");
+      k_push_tail_after<W><<<gp, kBlock, 0, s>>>(
+          fl_[S.fc].as<int32_t>(), S.nf, kPfxH, g_.rowptr, g_.col, R, codes, code_from, O,
+          done_.as<uint32_t>(), fbm_tile_.as<uint32_t>(), anyvis_.as<uint32_t>(), ctr_.as<Ctr>(),
+          slabF<W>(rows));
+      MSBFS_HIP_CHECK(hipGetLastError());
+      rows += gp;
+      S.push_after = false;
+    }
     S.have_active = S.level < S.stop_level;
   } else if (S.nact) {
     if (pfx) {

@@ -231,7 +231,8 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
     const int64_t t0 = tile_at(c), t1 = tile_at(c + 1);
     if (t1 > t0) {
       if (rows + grid > 3 * kMaxGrid) fail("tiled pull: counter slab rows exhausted");
-      auto kt = !small_bt ? k_pfx_tiles<W, kTileBlock, 1>
+      auto kt = S.push_after ? k_pfx_tiles<W, kTileBlock, 1, false>
+                : !small_bt ? k_pfx_tiles<W, kTileBlock, 1>
                 : tun_.tiles_bpc == 5 ? k_pfx_tiles<W, 256, 5> : k_pfx_tiles<W, 256, 4>;
       kt<<<grid, small_bt ? 256 : kTileBlock, 0, s>>>(
           T->tiles.as<PfxTile>() + t0, t1 - t0, T->pent.as<uint32_t>(), S.nparts, g_.rowptr, R,

@@ -260,7 +260,9 @@ def test_bitpar_tiled_first_pull(msbfs_pkg, K):
     runs = {"tiles": {}, "plain": {"tiles": 0}, "nocodes": {"codes": 0},
             "fewcodes": {"tiles_code_deg": 1}, "manycodes": {"tiles_code_deg": 400},
             "td3": {"dirs": "TBT"}, "td3plain": {"dirs": "TBT", "tiles": 0},
-            "bt256": {"tiles_bt": 256}, "bt256x4": {"tiles_bt": 256, "tiles_bpc": 4}}
+            "bt256": {"tiles_bt": 256}, "bt256x4": {"tiles_bt": 256, "tiles_bpc": 4},
+            "pushbefore": {"push_after": 0}, "td3pushbefore": {"dirs": "TBT", "push_after": 0},
+            "pushafter_nocodes": {"push_after": 1, "codes": 0}}
     out = {}
     for name, tun in runs.items():
         with m.Solver(g, "bitpar", max_groups=qs.K, tuning=tun) as s:
