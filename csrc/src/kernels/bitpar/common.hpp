@@ -127,6 +127,49 @@ __device__ __forceinline__ void wave_set_bits(uint32_t* bm, int32_t v, bool pred
   }
   if ((pending >> lane) & 1ull) atomicOr(&bm[w], bit);
 }
+// Bitmap bits of the group leaders (lanes 0, G, 2G, ...; pred only there) of a wave with few
+// vertices (G >= 8: at most 8 leaders): the leaders' ids are read into scalar registers one by
+// one, runs of ids in one 32-bit word are merged, and lane 0 issues one atomicOr per run. The
+// pull lists come from k_build_active in id order, so a wave's 8 vertices usually fall in one
+// or two words: ~2 atomics per wave instead of up to 8 (k_bu_first at RMAT-26 level 4 sets
+// 24.4M done bits; device-scope atomics execute at the memory side, tens of G/s chip-wide).
+template <int G>
+__device__ __forceinline__ void leader_set_bits(uint32_t* bm, int32_t v, bool pred) {
+  static_assert(G >= 8, "at most 8 leaders");
+  uint64_t m = __ballot(pred);
+  if (!m) return;
+  const bool l0 = lane_id() == 0;
+  uint32_t cw = 0xFFFFFFFFu, cm = 0u;  // (uniform: SGPRs)
+  while (m) {
+    const int l = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    const uint32_t vl = (uint32_t)__builtin_amdgcn_readlane(v, l);
+    const uint32_t w = vl >> 5, b = 1u << (vl & 31);
+    if (w != cw) {
+      if (cm && l0) atomicOr(&bm[cw], cm);
+      cw = w;
+      cm = b;
+    } else {
+      cm |= b;
+    }
+  }
+  if (l0) atomicOr(&bm[cw], cm);
+}
+// flags of the unfiltered pull kernels (k_bu_first, k_bu_full, k_bu_lean)
+constexpr int kFlagSkipRows = 1;     // dskip: a vertex finishing here writes no row
+constexpr int kFlagLeaderBits = 2;   // bitmap bits through leader_set_bits (G >= 8)
+// the pull kernels' bitmap bits: leader_set_bits where the wave has few vertices and the flag
+// is set, else wave_set_bits
+template <int G, bool COMBINE>
+__device__ __forceinline__ void set_bits_g(uint32_t* bm, int32_t v, bool pred, int flags) {
+  if constexpr (G >= 8) {
+    if (flags & kFlagLeaderBits) {
+      leader_set_bits<G>(bm, v, pred);
+      return;
+    }
+  }
+  wave_set_bits<COMBINE>(bm, v, pred);
+}
 // anyvis: bit v set once vertex v is visited by any group. A clear bit guarantees both visited
 // buffers of v are all-zero (bits are set before/with the first non-zero store and never
 // cleared within a batch), so pulls may skip the 8*W-byte load; a set bit only costs a load.

@@ -575,7 +575,8 @@ __global__ __launch_bounds__(kBlock, W >= 16 ? 8 : 6) void k_bu_first(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF, const int32_t* first,
-    const uint32_t* dsnap, int skip) {
+    const uint32_t* dsnap, int flags) {
+  const bool skip = flags & kFlagSkipRows;
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   // done / any-visited bits: one atomic per word of the wave (wave_set_bits) where a wave
@@ -641,9 +642,9 @@ __global__ __launch_bounds__(kBlock, W >= 16 ? 8 : 6) void k_bu_first(
     const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
     const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
     const bool leader = valid && slot == 0;
-    wave_set_bits<kCombine>(done, v, leader && fin);
+    set_bits_g<G, kCombine>(done, v, leader && fin, flags);
     if (leader && g_new) ef += deg;
-    wave_set_bits<kCombine>(anyvis, v, leader && g_first);
+    set_bits_g<G, kCombine>(anyvis, v, leader && g_first, flags);
     if (leader && g_first) ev += deg;
     q_push(qo, leader && !fin, v);
     q_push(qf, leader && g_new, v);

@@ -202,8 +202,9 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
     const uint64_t* R, uint64_t* Wb, int64_t n, const uint64_t* alive, const uint64_t* gmask,
     uint32_t* done, int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* actw2,
     int next_wide, uint32_t* slabF, const uint32_t* nact_dev, BuGate gate,
-    const uint32_t* dsnap, int skip) {
+    const uint32_t* dsnap, int flags) {
   if (!bu_gate_open(gate)) return;  // (uniform)
+  const bool skip = flags & kFlagSkipRows;
   if (nact_dev) nact = (int64_t)*nact_dev;
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   uint32_t na = 0, nf = 0, nw = 0;  // (wave-uniform)
   const RowBuf<W> rR = row_buf<W>(R, n), rO = row_buf<W>(Wb, n);
   const int voff = slot * VW * 8;
-  const int32_t zrow = (int32_t)n, srow = (int32_t)n + 1;  // all-zero row, scratch row
+  const int32_t zrow = (int32_t)n;  // the all-zero row
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
@@ -422,12 +423,13 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
     const uint64_t bn = __ballot(anynew), bf = __ballot(notfull);
     const bool g_new = (bn >> (sub * G)) & L::GBITS;
     const bool g_nf = (bf >> (sub * G)) & L::GBITS;
-    {  // also when nothing is open: Wb may hold the previous batch's rows (idle lanes: scratch row)
-      // (skip: a vertex done now is never read again, see above)
+    {  // also when nothing is open: Wb may hold the previous batch's rows
+      // (skip: a vertex done now is never read again, see above; a store under a branch costs
+      // no wait, and no idle lane hammers the scratch row's one cache line)
       V<VW> nv;
 #pragma unroll
       for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nwv.w[j];
-      st_row<W, VW>(rO, valid && (g_nf || !skip) ? v : srow, voff, nv);
+      if (valid && (g_nf || !skip)) st_row<W, VW>(rO, v, voff, nv);
     }
     bc.add(nwv);  // (zero for invalid lanes)
     if (++nadd == (1 << decltype(bc)::D) - 1) {
@@ -435,13 +437,13 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
       nadd = 0;
     }
     const bool leader = valid && slot == 0;
-    wave_set_bits<kCombine>(done, v, leader && !g_nf);
+    set_bits_g<G, kCombine>(done, v, leader && !g_nf, flags);
     const bool keep = leader && g_nf, app = leader && g_new;
     if (keep) eu += deg;
     if (app) ef += deg;
     {
       const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
-      wave_set_bits<kCombine>(anyvis, v, leader && g_first);
+      set_bits_g<G, kCombine>(anyvis, v, leader && g_first, flags);
       if (leader && g_first) ev += deg;
     }
     // third stage: the done probe of the next tile's first-step ids (loaded during this tile)
@@ -482,7 +484,8 @@ __global__ __launch_bounds__(kBlock, (lean_occ<W, U>())) void k_bu_lean(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, int64_t n, const uint64_t* alive, const uint64_t* gmask,
     uint32_t* done, int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF,
-    const int32_t* first, const uint32_t* dsnap, int skip) {
+    const int32_t* first, const uint32_t* dsnap, int flags) {
+  const bool skip = flags & kFlagSkipRows;
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
   constexpr int WT = U * VPW;  // list entries per wave and iteration
@@ -570,9 +573,9 @@ __global__ __launch_bounds__(kBlock, (lean_occ<W, U>())) void k_bu_lean(
       const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
       const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
       const bool leader = valid[k] && slot == 0;
-      wave_set_bits<kCombine>(done, v[k], leader && fin);
+      set_bits_g<G, kCombine>(done, v[k], leader && fin, flags);
       if (leader && g_new) ef += deg[k];
-      wave_set_bits<kCombine>(anyvis, v[k], leader && g_first);
+      set_bits_g<G, kCombine>(anyvis, v[k], leader && g_first, flags);
       if (leader && g_first) ev += deg[k];
       wq_push(qo, nqo, leader && !fin, v[k]);
       wq_push(qf, nqf, leader && g_new, v[k]);

@@ -89,15 +89,15 @@ struct Tuning {
   // lean pass kernel: 0 = k_bu_first (one tile per wave and iteration), 2 / 4 = k_bu_lean with
   // that many tiles per wave in flight (bitpar/pull_full.hpp)
   int first_u = 0;
-  // block size of the tiled first pull (1024: hub bitmap in LDS; 256: global hub probes, four
-  // or five blocks per CU; see k_pfx_tiles). Measured (RMAT-26 / 1024 groups, level 2): 12.5 ms
-  // at 1024, 14.1 ms at 256 x 4, 15.4 ms at 256 x 5 (96 VGPRs, spills): the L2 round trip of
-  // the probes costs more than the extra waves hide
-  int tiles_bt = 1024;
   // tiled first pull level: the tail push after the tiles, into the output rows (one GPU, no
   // chunked exchange; k_push_tail_after) instead of into acc rows every tile vertex reads
   // (RMAT-26 / 1024 groups: level 2 12.5 -> 10.95 ms, 20.7-21.3 -> 19.1-19.8 ms per step)
   int push_after = 1;
+  // done / any-visited bits of the 8-vertex waves (16 words) of the unfiltered pulls through
+  // leader_set_bits (one atomic per word run) instead of one atomic per vertex
+  int lbits = 0;
+  // dskip on the non-lean unfiltered full pulls too (RMAT-26 level 3; see level_bu)
+  int dskip3 = 0;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->

@@ -142,14 +142,14 @@ __device__ __forceinline__ void tile_mask_or(uint32_t* bm, int32_t v0, uint32_t 
 }
 
 // zrow: an all-zero row (the gather target of the idle lane groups of a batch)
-// BT = kTileBlock: one 1024-thread block per CU with the hub bitmap in LDS (4 waves per SIMD,
-// bound by the LDS). BT = 256 (tuning key tiles_bt): the hub probes read the global bitmap
-// (56 KB, L2-resident) instead, which leaves the LDS to the waves' accumulator rows: BPC
-// (tuning key tiles_bpc: 4 or 5) 256-thread blocks per CU, i.e. BPC waves per SIMD.
+// (One 1024-thread block per CU, bound by the LDS: the hub bitmap plus 16 waves' accumulator
+// rows. Measured round 4: 256-thread blocks probing the global, L2-resident hub bitmap instead,
+// 4 or 5 blocks per CU, ran level 2 in 14.1 / 15.4 ms against 12.5 ms here: the L2 round trip
+// of every probe costs more than the extra waves hide.)
 // ACC = false (tuning key push_after): the tail push runs after this kernel and ORs its bits
 // into the output rows itself (k_push_tail_after), so no acc row is read here.
-template <int W, int BT = kTileBlock, int BPC = 1, bool ACC = true>
-__global__ __launch_bounds__(BT, BPC) void k_pfx_tiles(
+template <int W, bool ACC = true>
+__global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
     const PfxTile* __restrict__ tiles, int64_t ntiles, const uint32_t* __restrict__ pent,
     int nparts, const int64_t* rowptr, const uint64_t* R, uint64_t* O, uint64_t* acc,
     const uint32_t* pvis, const uint32_t* snap, const uint32_t* code, int32_t code_from,
@@ -158,21 +158,19 @@ __global__ __launch_bounds__(BT, BPC) void k_pfx_tiles(
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, S = 64 / G, VT = kTileVT;
   static_assert(VPW <= kTileVT && kTileVT % VPW == 0, "whole epilogue passes per tile");
-  constexpr int NWV = BT / 64;
-  constexpr bool HUB_LDS = BT == kTileBlock;
-  constexpr int PB = HUB_LDS ? 4 : 2;  // rows in flight per lane group and batch
+  constexpr int NWV = kTileBlock / 64;
+  constexpr int PB = 4;       // rows in flight per lane group and batch
   constexpr int Q = kRoundQ;
   constexpr int CR = 65;      // bank-skewed counter rows (BitCounter::spill_strided)
   constexpr int YW = VT * W + 64;  // + one dummy word per lane (idle lanes' ORs, no conflicts)
-  __shared__ uint32_t hub[HUB_LDS ? kTileHubW : 1];
+  __shared__ uint32_t hub[kTileHubW];
   __shared__ unsigned long long Y[NWV][YW];
   __shared__ uint32_t lst[NWV][kRound];
   __shared__ uint32_t cnt[CR * W];
   __shared__ unsigned long long scratch[NWV];
   __shared__ uint32_t scratch32[NWV];
-  if constexpr (HUB_LDS)
-    for (int i = threadIdx.x; i < kTileHubW; i += BT) hub[i] = pvis[i];
-  for (int i = threadIdx.x; i < CR * W; i += BT) cnt[i] = 0;
+  for (int i = threadIdx.x; i < kTileHubW; i += kTileBlock) hub[i] = pvis[i];
+  for (int i = threadIdx.x; i < CR * W; i += kTileBlock) cnt[i] = 0;
   __syncthreads();
   const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
   unsigned long long* y = Y[wv];
@@ -186,7 +184,7 @@ __global__ __launch_bounds__(BT, BPC) void k_pfx_tiles(
   uint32_t nfc = 0;
   // 5 slices: a spill (one LDS add per set counter bit, ~100 per lane at level 2) every 31
   // passes (6 slices do not fit the 128 VGPRs of a 1024-thread block at 16 words)
-  BitCounter<VW, HUB_LDS ? 5 : 4> bc;
+  BitCounter<VW, 5> bc;
   bc.zero();
   int nadd = 0;
   const int64_t nwaves = (int64_t)gridDim.x * NWV;
@@ -202,7 +200,7 @@ __global__ __launch_bounds__(BT, BPC) void k_pfx_tiles(
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const uint32_t u = pk[q] != kPentNone ? pk[q] & kPentUMask : 0u;
-      const bool hit = ((HUB_LDS ? hub[u >> 5] : pvis[u >> 5]) >> (u & 31)) & 1u;
+      const bool hit = (hub[u >> 5] >> (u & 31)) & 1u;
       pk[q] = hit ? pk[q] : kPentNone;
     }
 #pragma unroll
@@ -415,7 +413,7 @@ __global__ __launch_bounds__(BT, BPC) void k_pfx_tiles(
   bc.template spill_strided32<CR>(cnt, slot);
   __syncthreads();
   uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
-  for (int i = threadIdx.x; i < 64 * W; i += BT) row[i] = cnt[i + (i >> 6)];
+  for (int i = threadIdx.x; i < 64 * W; i += kTileBlock) row[i] = cnt[i + (i >> 6)];
 }
 
 // frontier list from the frontier bitmap (LDS block queue; rare: only when a top-down level

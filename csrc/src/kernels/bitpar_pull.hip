@@ -222,9 +222,19 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                         !tiled && !pfx && S.bu_levels >= tun_.lean_level &&
                         S.nact >= tun_.lean_min;
   const bool skip_now = lean_now && !COUNT && tun_.dskip && tun_.full && !S.keep_rows;
-  const uint32_t* dsnap = (!COUNT && tun_.full) ? done_probe(S, skip_now, s) : nullptr;
-  S.skip_pending = skip_now;
+  // dskip3: the full pull of an unfiltered, non-lean level (RMAT-26 level 3) skips the rows of
+  // the vertices it finishes too, but probes nothing itself while no earlier level skipped (its
+  // input rows are all current); the later levels probe as after any skipping level
+  const bool skip3 = !lean_now && tun_.dskip3 && tun_.dskip && !COUNT && tun_.full &&
+                     !S.keep_rows && filter_from == INT32_MAX && !tiled && !pfx &&
+                     S.bu_levels >= 1;
+  const bool probed_before = S.skipped_any;
+  const uint32_t* dsnap =
+      (!COUNT && tun_.full) ? done_probe(S, skip_now || skip3, s) : nullptr;
+  const uint32_t* dprobe = skip3 && !probed_before ? nullptr : dsnap;
+  S.skip_pending = skip_now || skip3;
   S.skip_alive = alive;
+  const int lb = tun_.lbits ? kFlagLeaderBits : 0;  // (see leader_set_bits)
   int32_t code_from = kNoCodes;
   const uint32_t* codes = nullptr;
   if (first_bu && S.level == 2 && tun_.codes && W >= 8 && S.ef0 > 0 && n <= INT32_MAX) {
@@ -317,14 +327,14 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
               act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
               done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
-              skip_now ? 1 : 0);
+              (skip_now ? kFlagSkipRows : 0) | lb);
         } else {
           gl = grid_for(S.nact, L::TILE, grid);
           k_bu_first<W><<<gl, kBlock, 0, s>>>(
               act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
               done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
-              skip_now ? 1 : 0);
+              (skip_now ? kFlagSkipRows : 0) | lb);
         }
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gl;
@@ -333,7 +343,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
               done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
-              slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{}, dsnap, skip_now ? 1 : 0);
+              slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{}, dsnap, (skip_now ? kFlagSkipRows : 0) | lb);
         else
           k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
@@ -349,7 +359,8 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                                  sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
                                  fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                  anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
-                                 slabF<W>(rows), nullptr, BuGate{}, dsnap, 0);
+                                 slabF<W>(rows), nullptr, BuGate{}, dprobe,
+                                 (skip3 ? kFlagSkipRows : 0) | lb);
         rows += gn;
       } else {
         auto kn = FUSE ? (filt ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, true>
@@ -401,12 +412,12 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
           desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
           sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-          coop, codes, code_from, snap, dsnap);
+          coop, codes, code_from, snap, dprobe);
     } else {
       k_bu_chunks<W, 256, kBlock, 0><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
           desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask,
           acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, coop, codes, code_from,
-          snap, dsnap);
+          snap, dprobe);
     }
     MSBFS_HIP_CHECK(hipGetLastError());
     const int gw = grid_for(S.nactw, L::TILE, grid);
@@ -493,7 +504,8 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
       k_bu_full<W, full_cs<W>(), 1><<<grid, kBlock, 0, s>>>(
           list, 0, g_.rowptr, g_.col, R, O, g_.n, alive, sm.gmask, done_.as<uint32_t>(),
           act_[p ^ 1].as<int32_t>(), fl_out, out, anyvis_.as<uint32_t>(),
-          actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate, dsnap, 0);
+          actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate, dsnap,
+          tun_.lbits ? kFlagLeaderBits : 0);
     else
       kn<<<grid, kBlock, 0, s>>>(list, 0, g_.rowptr, g_.col, R, O, alive, sm.gmask,
                                  done_.as<uint32_t>(), act_[p ^ 1].as<int32_t>(), fl_out, out,

@@ -45,25 +45,19 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "tiles_code_deg") tiles_code_deg = to_num(key, v);
   else if (key == "full") full = (int)to_num(key, v);
   else if (key == "dskip") dskip = (int)to_num(key, v);
-  else if (key == "tiles_bt") {
-    tiles_bt = (int)to_num(key, v);
-    if (tiles_bt != 1024 && tiles_bt != 256) fail("tuning: tiles_bt must be 1024 or 256");
-  } else if (key == "tiles_bpc") {
-    tiles_bpc = (int)to_num(key, v);
-    if (tiles_bpc != 4 && tiles_bpc != 5) fail("tuning: tiles_bpc must be 4 or 5");
-  } else if (key == "push_after") {
-    push_after = (int)to_num(key, v);
-  } else if (key == "first_u") {
+  else if (key == "push_after") push_after = (int)to_num(key, v);
+  else if (key == "dskip3") dskip3 = (int)to_num(key, v);
+  else if (key == "lbits") lbits = (int)to_num(key, v);
+  else if (key == "first_u") {
     first_u = (int)to_num(key, v);
     if (first_u != 0 && first_u != 2 && first_u != 4) fail("tuning: first_u must be 0, 2 or 4");
-  }
-  else if (key == "dirs") {
+  } else if (key == "dirs") {
     for (char c : v)
       if (c != 'T' && c != 'B' && c != '.') fail("tuning: dirs takes T, B or . per level");
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip first_u tiles_bt tiles_bpc push_after dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip first_u push_after lbits dskip3 dirs)");
   }
 }
 

@@ -198,8 +198,7 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
   const int64_t nwords = (g_.n + 31) / 32;
   MSBFS_HIP_CHECK(hipMemsetAsync(fbm_tile_.p, 0, (size_t)nwords * sizeof(uint32_t), s));
   const uint32_t* pvis = snap ? snap : anyvis_.as<uint32_t>();
-  const bool small_bt = tun_.tiles_bt == 256;
-  const int grid = std::max(1, num_cus_) * (small_bt ? tun_.tiles_bpc : 1);
+  const int grid = std::max(1, num_cus_);
   // tile ranges: one launch for the whole level, or one per own-vertex range of a chunked
   // hybrid phase A (each range's rows are final once its launch and, for the first, the big
   // vertices' finalize ran; on_chunk then packs and sends them while the next range computes)
@@ -231,10 +230,8 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
     const int64_t t0 = tile_at(c), t1 = tile_at(c + 1);
     if (t1 > t0) {
       if (rows + grid > 3 * kMaxGrid) fail("tiled pull: counter slab rows exhausted");
-      auto kt = S.push_after ? k_pfx_tiles<W, kTileBlock, 1, false>
-                : !small_bt ? k_pfx_tiles<W, kTileBlock, 1>
-                : tun_.tiles_bpc == 5 ? k_pfx_tiles<W, 256, 5> : k_pfx_tiles<W, 256, 4>;
-      kt<<<grid, small_bt ? 256 : kTileBlock, 0, s>>>(
+      auto kt = S.push_after ? k_pfx_tiles<W, false> : k_pfx_tiles<W, true>;
+      kt<<<grid, kTileBlock, 0, s>>>(
           T->tiles.as<PfxTile>() + t0, t1 - t0, T->pent.as<uint32_t>(), S.nparts, g_.rowptr, R,
           O, acc_[S.ac].as<uint64_t>(), pvis, snap, codes, codes ? code_from : INT32_MAX, alive,
           sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), fbm_tile_.as<uint32_t>(),
