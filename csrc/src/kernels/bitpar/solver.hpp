@@ -94,10 +94,13 @@ struct Tuning {
   // (RMAT-26 / 1024 groups: level 2 12.5 -> 10.95 ms, 20.7-21.3 -> 19.1-19.8 ms per step)
   int push_after = 1;
   // done / any-visited bits of the 8-vertex waves (16 words) of the unfiltered pulls through
-  // leader_set_bits (one atomic per word run) instead of one atomic per vertex
+  // leader_set_bits (one atomic per word run) instead of one atomic per vertex. Measured slower
+  // (RMAT-26 / 1024 groups: level 4 1.73 -> 1.92 ms, level 3 5.80 -> 5.90 ms): the scalar loop
+  // costs more than the atomics it saves, which are not what bounds these kernels
   int lbits = 0;
-  // dskip on the non-lean unfiltered full pulls too (RMAT-26 level 3; see level_bu)
-  int dskip3 = 0;
+  // dskip on the non-lean unfiltered full pulls too (RMAT-26 level 3: 5.80 -> 5.68 ms, 1 GB of
+  // row stores fewer; see level_bu)
+  int dskip3 = 1;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->
