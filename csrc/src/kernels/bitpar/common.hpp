@@ -127,49 +127,10 @@ __device__ __forceinline__ void wave_set_bits(uint32_t* bm, int32_t v, bool pred
   }
   if ((pending >> lane) & 1ull) atomicOr(&bm[w], bit);
 }
-// Bitmap bits of the group leaders (lanes 0, G, 2G, ...; pred only there) of a wave with few
-// vertices (G >= 8: at most 8 leaders): the leaders' ids are read into scalar registers one by
-// one, runs of ids in one 32-bit word are merged, and lane 0 issues one atomicOr per run. The
-// pull lists come from k_build_active in id order, so a wave's 8 vertices usually fall in one
-// or two words: ~2 atomics per wave instead of up to 8 (k_bu_first at RMAT-26 level 4 sets
-// 24.4M done bits; device-scope atomics execute at the memory side, tens of G/s chip-wide).
-template <int G>
-__device__ __forceinline__ void leader_set_bits(uint32_t* bm, int32_t v, bool pred) {
-  static_assert(G >= 8, "at most 8 leaders");
-  uint64_t m = __ballot(pred);
-  if (!m) return;
-  const bool l0 = lane_id() == 0;
-  uint32_t cw = 0xFFFFFFFFu, cm = 0u;  // (uniform: SGPRs)
-  while (m) {
-    const int l = __ffsll((unsigned long long)m) - 1;
-    m &= m - 1;
-    const uint32_t vl = (uint32_t)__builtin_amdgcn_readlane(v, l);
-    const uint32_t w = vl >> 5, b = 1u << (vl & 31);
-    if (w != cw) {
-      if (cm && l0) atomicOr(&bm[cw], cm);
-      cw = w;
-      cm = b;
-    } else {
-      cm |= b;
-    }
-  }
-  if (l0) atomicOr(&bm[cw], cm);
-}
 // flags of the unfiltered pull kernels (k_bu_first, k_bu_full, k_bu_lean)
 constexpr int kFlagSkipRows = 1;     // dskip: a vertex finishing here writes no row
-constexpr int kFlagLeaderBits = 2;   // bitmap bits through leader_set_bits (G >= 8)
-// the pull kernels' bitmap bits: leader_set_bits where the wave has few vertices and the flag
-// is set, else wave_set_bits
-template <int G, bool COMBINE>
-__device__ __forceinline__ void set_bits_g(uint32_t* bm, int32_t v, bool pred, int flags) {
-  if constexpr (G >= 8) {
-    if (flags & kFlagLeaderBits) {
-      leader_set_bits<G>(bm, v, pred);
-      return;
-    }
-  }
-  wave_set_bits<COMBINE>(bm, v, pred);
-}
+constexpr int kFlagHitSkip = 4;      // k_bu_first: done first neighbour -> finished, row unread
+constexpr int kFlagCountRem = 8;     // k_bu_full: count the groups still unvisited, not new ones
 // anyvis: bit v set once vertex v is visited by any group. A clear bit guarantees both visited
 // buffers of v are all-zero (bits are set before/with the first non-zero store and never
 // cleared within a batch), so pulls may skip the 8*W-byte load; a set bit only costs a load.
@@ -354,13 +315,20 @@ __device__ __forceinline__ bool bu_gate_open(const BuGate& g) {
 // Sum the level's slab rows: block (word, row-group); lane = group bit. F += level * count
 // (`level` is the weight: 0 for a level another rank of the hybrid mode accounts for),
 // alive_next |= groups with count > 0 (one ballot + one atomicOr per word per row-group).
+// cum[i] (when not null) = vertices with edges visited by group i so far (see k_init), kept for
+// the subtractive count: with npos >= 0 (one row group: a block owns its word) the slab rows
+// hold, per group, the vertices still NOT visited after the level (the hit-skip lean level, see
+// k_bu_first), and the level's new count is (npos - cum[i]) - that, for the groups alive
+// (alive_cur) at the level; npos = vertices with edges.
 template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
                                                          const unsigned long long* slabE, int rows,
                                                          int rgroups, unsigned long long* F,
                                                          unsigned long long* E,
                                                          uint64_t* alive_next, uint32_t level,
-                                                         BuGate gate) {
+                                                         BuGate gate, unsigned long long* cum,
+                                                         const uint64_t* alive_cur,
+                                                         long long npos) {
   if (!bu_gate_open(gate)) return;  // (uniform: no barrier skipped by part of the block)
   __shared__ unsigned long long pf[kWaves][64], pe[kWaves][64];
   const int word = blockIdx.x % W, rg = blockIdx.x / W;
@@ -381,6 +349,12 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
       f += pf[w][lane];
       e += pe[w][lane];
     }
+    if (npos >= 0) {  // (subtractive level: rgroups == 1)
+      const bool alv = (alive_cur[word] >> lane) & 1ull;
+      const unsigned long long c = cum[i];
+      f = alv ? (unsigned long long)npos - c - f : 0ull;
+    }
+    if (cum && f) atomicAdd(&cum[i], f);  // (several row groups per group i)
     if (f) atomicAdd(&F[i], f * level);
     if constexpr (COUNT) {
       if (e) atomicAdd(&E[i], e);
@@ -400,14 +374,15 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce_multi(const uint32_t* s
                                                                int nlev, int rgroups,
                                                                uint32_t level_first, int weight_l1,
                                                                unsigned long long* F,
-                                                               uint64_t* alive_next) {
+                                                               uint64_t* alive_next,
+                                                               unsigned long long* cum) {
   __shared__ uint32_t pl[kWaves][64];
   const int word = blockIdx.x % W, rg = blockIdx.x / W;
   const int lane = lane_id(), wv = threadIdx.x >> 6;
   const int r0 = (int)((int64_t)rows * rg / rgroups);
   const int r1 = (int)((int64_t)rows * (rg + 1) / rgroups);
   const int i = word * 64 + lane;
-  unsigned long long fw = 0;
+  unsigned long long fw = 0, fc = 0;
   for (int j = 0; j < nlev; ++j) {
     uint32_t f = 0;
     for (int r = r0 + wv; r < r1; r += kWaves) f += slabF[((size_t)j * rows + r) * (64 * W) + i];
@@ -417,12 +392,14 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce_multi(const uint32_t* s
       for (int w = 1; w < kWaves; ++w) f += pl[w][lane];
       const uint32_t lvl = level_first + (uint32_t)j;
       fw += (unsigned long long)f * ((lvl == 1 && !weight_l1) ? 0u : lvl);
+      fc += f;
       const uint64_t m = __ballot(f != 0);
       if (lane == 0 && m) atomicOr((unsigned long long*)&alive_next[16 * j + word], m);
     }
     __syncthreads();
   }
   if (wv == 0 && fw) atomicAdd(&F[i], fw);
+  if (wv == 0 && fc && cum) atomicAdd(&cum[i], fc);
 }
 
 // ---------------------------------------------------------------------------------------------

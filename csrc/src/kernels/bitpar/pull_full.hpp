@@ -431,19 +431,26 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
       for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nwv.w[j];
       if (valid && (g_nf || !skip)) st_row<W, VW>(rO, v, voff, nv);
     }
-    bc.add(nwv);  // (zero for invalid lanes)
+    if (flags & kFlagCountRem) {  // (uniform; the overflow of a hit-skip lean pass)
+      V<VW> rem;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) rem.w[j] = unv.w[j] & ~nwv.w[j];
+      bc.add(rem);
+    } else {
+      bc.add(nwv);  // (zero for invalid lanes)
+    }
     if (++nadd == (1 << decltype(bc)::D) - 1) {
       bc.template spill_strided32<CR>(cnt, slot);
       nadd = 0;
     }
     const bool leader = valid && slot == 0;
-    set_bits_g<G, kCombine>(done, v, leader && !g_nf, flags);
+    wave_set_bits<kCombine>(done, v, leader && !g_nf);
     const bool keep = leader && g_nf, app = leader && g_new;
     if (keep) eu += deg;
     if (app) ef += deg;
     {
       const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
-      set_bits_g<G, kCombine>(anyvis, v, leader && g_first, flags);
+      wave_set_bits<kCombine>(anyvis, v, leader && g_first);
       if (leader && g_first) ev += deg;
     }
     // third stage: the done probe of the next tile's first-step ids (loaded during this tile)
@@ -573,9 +580,9 @@ __global__ __launch_bounds__(kBlock, (lean_occ<W, U>())) void k_bu_lean(
       const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
       const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
       const bool leader = valid[k] && slot == 0;
-      set_bits_g<G, kCombine>(done, v[k], leader && fin, flags);
+      wave_set_bits<kCombine>(done, v[k], leader && fin);
       if (leader && g_new) ef += deg[k];
-      set_bits_g<G, kCombine>(anyvis, v[k], leader && g_first, flags);
+      wave_set_bits<kCombine>(anyvis, v[k], leader && g_first);
       if (leader && g_first) ev += deg[k];
       wq_push(qo, nqo, leader && !fin, v[k]);
       wq_push(qf, nqf, leader && g_new, v[k]);

@@ -93,14 +93,13 @@ struct Tuning {
   // chunked exchange; k_push_tail_after) instead of into acc rows every tile vertex reads
   // (RMAT-26 / 1024 groups: level 2 12.5 -> 10.95 ms, 20.7-21.3 -> 19.1-19.8 ms per step)
   int push_after = 1;
-  // done / any-visited bits of the 8-vertex waves (16 words) of the unfiltered pulls through
-  // leader_set_bits (one atomic per word run) instead of one atomic per vertex. Measured slower
-  // (RMAT-26 / 1024 groups: level 4 1.73 -> 1.92 ms, level 3 5.80 -> 5.90 ms): the scalar loop
-  // costs more than the atomics it saves, which are not what bounds these kernels
-  int lbits = 0;
   // dskip on the non-lean unfiltered full pulls too (RMAT-26 level 3: 5.80 -> 5.68 ms, 1 GB of
   // row stores fewer; see level_bu)
   int dskip3 = 1;
+  // hit-skip lean pass: a vertex whose first neighbour was done at the level start finishes
+  // without its own row being read; the level counts the vertices still unvisited per group
+  // afterwards instead of the new ones (k_bu_first, k_level_reduce)
+  int hskip = 0;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->
@@ -172,7 +171,9 @@ class BitparSolver final : public Solver {
     // dskip: the last level skipped the rows of the vertices it finished; a push level next
     // restores those of its frontier (k_fix_done_rows) from the read buffer and this alive mask
     bool keep_rows = false;
-    bool push_after = false;  // this tiled level's tail push runs after the tiles (k_push_tail_after)             // every row written (hybrid phase A packs them)
+    bool push_after = false;
+    bool cum_ok = false;      // Small::cum counts every level of this run (not hybrid phase C)
+    bool sub_reduce = false;  // this level's slab rows hold not-visited counts (hit-skip lean pass)  // this tiled level's tail push runs after the tiles (k_push_tail_after)             // every row written (hybrid phase A packs them)
     bool skip_pending = false;
     const uint64_t* skip_alive = nullptr;
     // a level skipped rows: every later pull level of the batch probes dsnap_ (re-snapshotted
@@ -184,6 +185,7 @@ class BitparSolver final : public Solver {
     unsigned long long* E;
     uint64_t* alive[2];
     uint64_t* gmask;
+    unsigned long long* cum;  // per group: vertices with edges visited so far (k_level_reduce)
   };
 
  private:
@@ -194,6 +196,7 @@ class BitparSolver final : public Solver {
     r.alive[0] = (uint64_t*)(r.E + 64 * 16);
     r.alive[1] = r.alive[0] + 16;
     r.gmask = r.alive[1] + 16;
+    r.cum = (unsigned long long*)(r.gmask + 32);
     return r;
   }
   template <int W>
@@ -298,6 +301,10 @@ class BitparSolver final : public Solver {
     return n_eff_;
   }
 
+  // vertices with deg > 0 (cached per graph buffers; the subtractive count of the hit-skip
+  // lean pass, bitpar_pull.hip)
+  int64_t npos(hipStream_t s);
+
   HostCtr read_ctr(hipStream_t s) {
     MSBFS_HIP_CHECK(hipMemcpyAsync(hctr_->p, ctr_.p, sizeof(Ctr), hipMemcpyDeviceToHost, s));
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
@@ -336,6 +343,8 @@ class BitparSolver final : public Solver {
   int32_t epoch_ = 0;
   int64_t n_eff_ = 0;
   const void* eff_key_[3] = {nullptr, nullptr, nullptr};
+  int64_t npos_ = -1;
+  const void* npos_key_[2] = {nullptr, nullptr};
   DevBuf plen_;
   DevBuf first_;
   DevBuf code_ws_;

@@ -71,6 +71,24 @@ int32_t BitparSolver::code_bound(double min_deg) {
   return deg_bounds_[k];
 }
 
+int64_t BitparSolver::npos(hipStream_t s) {
+  if (npos_key_[0] != (const void*)g_.rowptr || npos_key_[1] != (const void*)g_.col) {
+    DevBuf c;
+    c.alloc(sizeof(unsigned long long));
+    MSBFS_HIP_CHECK(hipMemsetAsync(c.p, 0, sizeof(unsigned long long), s));
+    k_count_wide<<<grid_for(g_.n, kBlock, 2048), kBlock, 0, s>>>(g_.rowptr, g_.n, 0,
+                                                                 c.as<unsigned long long>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+    unsigned long long h = 0;
+    MSBFS_HIP_CHECK(hipMemcpyAsync(&h, c.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    npos_ = (int64_t)h;
+    npos_key_[0] = g_.rowptr;
+    npos_key_[1] = g_.col;
+  }
+  return npos_;
+}
+
 // Everything a run would otherwise build or allocate on first use, so that no timed run pays
 // for it (the CLI's computation phase, main.cu:301-400): the vertex extent, the prefix
 // lengths and first-neighbour array, the degree-bound table, and the worst-case chunk
@@ -83,6 +101,7 @@ void BitparSolver::prepare(hipStream_t s) {
     if (maxW_ >= 8) (void)pfx_tiles(maxW_, 0, 1, s);  // (the first pull level's tiles)
   }
   if (tun_.lean) first_nbr(s);
+  (void)npos(s);
   (void)code_bound(1.0);
   DevBuf c;
   c.alloc(sizeof(unsigned long long));
@@ -234,7 +253,6 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   const uint32_t* dprobe = skip3 && !probed_before ? nullptr : dsnap;
   S.skip_pending = skip_now || skip3;
   S.skip_alive = alive;
-  const int lb = tun_.lbits ? kFlagLeaderBits : 0;  // (see leader_set_bits)
   int32_t code_from = kNoCodes;
   const uint32_t* codes = nullptr;
   if (first_bu && S.level == 2 && tun_.codes && W >= 8 && S.ef0 > 0 && n <= INT32_MAX) {
@@ -318,7 +336,12 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       if (tun_.lean && !S.lean_off && FUSE && !filt && S.bu_levels >= tun_.lean_level &&
           S.nact >= tun_.lean_min) {
         S.lean_ran = true;
-        // lean first pass, then the regular pull over the vertices it could not finish
+        // lean first pass, then the regular pull over the vertices it could not finish.
+        // hit-skip (tuning hskip): see k_bu_first; the level's counts become subtractive
+        // (every active vertex is on the narrow list and every level so far fed Small::cum)
+        const bool hs = tun_.hskip && skip_now && dsnap && tun_.full && !tun_.first_u &&
+                        S.nactw == 0 && S.cum_ok;
+        S.sub_reduce = hs;
         int gl;
         if (tun_.first_u) {
           gl = grid_for(S.nact, L::TILE * tun_.first_u, grid);
@@ -327,14 +350,15 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
               act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
               done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
-              (skip_now ? kFlagSkipRows : 0) | lb);
+              (skip_now ? kFlagSkipRows : 0));
         } else {
           gl = grid_for(S.nact, L::TILE, grid);
-          k_bu_first<W><<<gl, kBlock, 0, s>>>(
+          auto kb = hs ? k_bu_first<W, true> : k_bu_first<W, false>;
+          kb<<<gl, kBlock, 0, s>>>(
               act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
               done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
-              (skip_now ? kFlagSkipRows : 0) | lb);
+              (skip_now ? kFlagSkipRows : 0) | (hs ? kFlagHitSkip : 0));
         }
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gl;
@@ -343,7 +367,8 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
               done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
-              slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{}, dsnap, (skip_now ? kFlagSkipRows : 0) | lb);
+              slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{}, dsnap,
+              (skip_now ? kFlagSkipRows : 0) | (hs ? kFlagCountRem : 0));
         else
           k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
@@ -360,7 +385,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                                  fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
                                  anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
                                  slabF<W>(rows), nullptr, BuGate{}, dprobe,
-                                 (skip3 ? kFlagSkipRows : 0) | lb);
+                                 (skip3 ? kFlagSkipRows : 0));
         rows += gn;
       } else {
         auto kn = FUSE ? (filt ? k_bu_narrow<W, COUNT, kBlock, 0, FUSE, true>
@@ -504,8 +529,7 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
       k_bu_full<W, full_cs<W>(), 1><<<grid, kBlock, 0, s>>>(
           list, 0, g_.rowptr, g_.col, R, O, g_.n, alive, sm.gmask, done_.as<uint32_t>(),
           act_[p ^ 1].as<int32_t>(), fl_out, out, anyvis_.as<uint32_t>(),
-          actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate, dsnap,
-          tun_.lbits ? kFlagLeaderBits : 0);
+          actw_[p ^ 1].as<int32_t>(), next_wide, slab, len, gate, dsnap, 0);
     else
       kn<<<grid, kBlock, 0, s>>>(list, 0, g_.rowptr, g_.col, R, O, alive, sm.gmask,
                                  done_.as<uint32_t>(), act_[p ^ 1].as<int32_t>(), fl_out, out,
@@ -526,7 +550,7 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
              &slots[i].actw2.v, gate, p);
     k_level_reduce<W, false><<<W * rg, kBlock, 0, s>>>(slabF<W>(0), slabE<W>(0), rows, rg, sm.F,
                                                        sm.E, aslot + 16 * (i + 1), level0 + 1 + i,
-                                                       gate);
+                                                       gate, sm.cum, nullptr, -1ll);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   MSBFS_HIP_CHECK(hipMemcpyAsync(hbctr_->p, bctr_.p, (size_t)(K + 1) * sizeof(Ctr),
