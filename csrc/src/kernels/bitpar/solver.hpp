@@ -98,7 +98,10 @@ struct Tuning {
   int dskip3 = 1;
   // hit-skip lean pass: a vertex whose first neighbour was done at the level start finishes
   // without its own row being read; the level counts the vertices still unvisited per group
-  // afterwards instead of the new ones (k_bu_first, k_level_reduce)
+  // afterwards instead of the new ones (k_bu_first, k_level_reduce). Exact, but measured slower
+  // (RMAT-26 / 1024 groups: level 4 1.72 -> 1.94 ms; 128 groups 0.67 -> 0.77 ms): few first
+  // neighbours are done at level 4 (late groups keep even the top hubs open), so most vertices
+  // take the longer chain (own row only after the probe)
   int hskip = 0;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a

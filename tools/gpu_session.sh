@@ -59,7 +59,7 @@ for s in "$@"; do
       PROF_START=k_init PROF_NTH=8 python tools/prof_summary.py gpurun_out/profhc \
         > gpurun_out/profhc_a0.md &&
       rm -f gpurun_out/profhc/run_kernel_trace.csv ;;
-    pmchbm) export TMPDIR=/tmp; R="k_bu|k_push|k_td|k_build|k_level"; rm -rf gpurun_out/pmch1 gpurun_out/pmch2 gpurun_out/pmch3
+    pmchbm) export TMPDIR=/tmp; R="${PMC_RE:-k_bu|k_push|k_pfx|k_build}"; rm -rf gpurun_out/pmch1 gpurun_out/pmch2 gpurun_out/pmch3
          step pmch1 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmch1 -o run -- python bench.py --steps 1 --warmup 0 --verify 0 &&
          step pmch2 300 rocprofv3 --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmch2 -o run -- python bench.py --steps 1 --warmup 0 --verify 0 &&
          step pmch3 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT TA_BUSY_avr --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmch3 -o run -- python bench.py --steps 1 --warmup 0 --verify 0 &&
