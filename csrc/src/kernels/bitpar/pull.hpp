@@ -958,6 +958,74 @@ static __global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl,
   }
 }
 
+// Two-pass chunk scheduling on the early-exit levels (tuning key chunk2): pass 1 pulls only the
+// first chunk of every wide vertex (most are covered by the hubs at the head of their sorted
+// rows), pass 2 only the remaining chunks of the vertices pass 1 left open. In one pass every
+// chunk of a covered vertex still cost its wave an own-row load and a returning atomic before
+// it could skip (RMAT-26 level 3: 313K wide vertices, ~1M+ chunks, 0.5 ms).
+static __global__ __launch_bounds__(kBlock) void k_chunk_first(const int32_t* wl, int64_t nw,
+                                                               const int64_t* rowptr,
+                                                               ChunkDesc* desc, int64_t* cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int32_t v = wl[i];
+    const int64_t b = rowptr[v], e = rowptr[v + 1];
+    desc[i] = ChunkDesc{v, (uint32_t)b, (uint32_t)((uint64_t)b >> 32),
+                        (int32_t)min((int64_t)kChunk, e - b)};
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *cnt = nw;
+}
+// chunks left of wide vertex i after pass 1: 0 once acc[v] (the union its chunks published)
+// covers every alive group v misses, else all but the first (G lanes per vertex)
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_chunk_rest_count(
+    const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, const uint64_t* acc,
+    const uint64_t* alive, const uint64_t* gmask, const uint32_t* snap, int64_t* cnt) {
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
+  const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
+  V<VW> am;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
+  for (int64_t tb = (int64_t)blockIdx.x * TILE; tb < nw; tb += (int64_t)gridDim.x * TILE) {
+    const int64_t i = tb + wv * VPW + sub;
+    bool open = false;
+    int32_t v = 0;
+    if (i < nw) {
+      v = wl[i];
+      const int64_t vo = (int64_t)v * W + slot * VW;
+      const V<VW> r = (snap && !any_visited(snap, v)) ? vzero<VW>() : ldv<VW>(R + vo);
+      const V<VW> a = ldv<VW>(acc + vo);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) open |= (~r.w[j] & am.w[j] & ~a.w[j]) != 0;
+    }
+    const bool g_open = (__ballot(open) >> (sub * G)) & L::GBITS;
+    if (i < nw && slot == 0) {
+      const int64_t d = rowptr[v + 1] - rowptr[v];
+      const int64_t nc = (d + kChunk - 1) / kChunk;
+      cnt[i] = g_open && nc > 1 ? nc - 1 : 0;
+    }
+  }
+}
+// descriptors of the pass-2 chunks (offs = inclusive prefix of k_chunk_rest_count)
+static __global__ __launch_bounds__(kBlock) void k_chunk_rest_desc(const int32_t* wl, int64_t nw,
+                                                                   const int64_t* offs,
+                                                                   const int64_t* rowptr,
+                                                                   ChunkDesc* desc) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t c0 = i ? offs[i - 1] : 0, c1 = offs[i];
+    if (c0 == c1) continue;
+    const int32_t v = wl[i];
+    const int64_t b = rowptr[v], e = rowptr[v + 1];
+    for (int64_t c = c0; c < c1; ++c) {
+      const int64_t cb = b + (1 + c - c0) * kChunk;
+      desc[c] = ChunkDesc{v, (uint32_t)cb, (uint32_t)((uint64_t)cb >> 32),
+                          (int32_t)min((int64_t)kChunk, e - cb)};
+    }
+  }
+}
+
 template <int W, int T, int BT, int HUBW>
 __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_bu_chunks(
     const ChunkDesc* __restrict__ desc, const int64_t* nchunks_p, const int32_t* col,

@@ -103,6 +103,8 @@ struct Tuning {
   // neighbours are done at level 4 (late groups keep even the top hubs open), so most vertices
   // take the longer chain (own row only after the probe)
   int hskip = 0;
+  // two-pass chunk scheduling of the wide vertices on early-exit levels (k_chunk_first)
+  int chunk2 = 0;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->
@@ -349,6 +351,7 @@ class BitparSolver final : public Solver {
   int64_t npos_ = -1;
   const void* npos_key_[2] = {nullptr, nullptr};
   DevBuf plen_;
+  DevBuf chunk_cnt_;  // pass-1 chunk count of the two-pass wide pull (device int64)
   DevBuf first_;
   DevBuf code_ws_;
   const void* first_key_[2] = {nullptr, nullptr};

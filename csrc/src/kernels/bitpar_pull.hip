@@ -404,7 +404,51 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     }
     MSBFS_HIP_CHECK(hipGetLastError());
   }
-  if (S.nactw && !tiled) {
+  // early exit across a vertex's chunks (coop) everywhere except on an explosive first
+  // bottom-up level (level 2: hardly any row gets covered, and round-robin chunk dealing
+  // balances the hubs better). When top-down ran longer (RMAT-30: first pull at level 3, most of
+  // every hub's groups already visited) the early exit skips most chunks.
+  const int coop = !first_bu || S.level != 2 ? 1 : 0;
+  auto launch_chunks = [&](const ChunkDesc* d, const int64_t* np, int64_t maxc) {
+    if (hub_lds) {
+      // exact chunk count = *np, read on the device (no host round trip); one block per CU
+      // with the 128-KB hub bitmap (ids < 1M) except on the prefix level, whose prefixes end
+      // at the small one's bound (two blocks per CU)
+      const bool big = hub_big && !pfx;
+      auto ck = big ? k_bu_chunks<W, 256, 1024, kHubBig> : k_bu_chunks<W, 256, 1024, kHubW>;
+      ck<<<grid_for(maxc, 16, big ? 256 : 512), 1024, 0, s>>>(
+          d, np, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(),
+          filter_from, coop, codes, code_from, snap, dprobe);
+    } else {
+      k_bu_chunks<W, 256, kBlock, 0><<<grid_for(maxc, kWaves, 8192), kBlock, 0, s>>>(
+          d, np, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(),
+          filter_from, coop, codes, code_from, snap, dprobe);
+    }
+    MSBFS_HIP_CHECK(hipGetLastError());
+  };
+  if (S.nactw && !tiled && coop && !pfx && tun_.chunk2) {
+    // two passes (see k_chunk_first): first chunks, then the rest of the open vertices
+    const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
+    desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
+    chunk_cnt_.ensure(sizeof(int64_t));
+    ChunkDesc* d = desc_.as<ChunkDesc>();
+    k_chunk_first<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
+        actw_[0].as<int32_t>(), S.nactw, g_.rowptr, d, chunk_cnt_.as<int64_t>());
+    MSBFS_HIP_CHECK(hipGetLastError());
+    launch_chunks(d, chunk_cnt_.as<int64_t>(), S.nactw);
+    int64_t* cnt = scan_tmp_.as<int64_t>();
+    char* t2 = (char*)scan_tmp_.p + (((size_t)S.nactw * sizeof(int64_t) + 255) & ~size_t(255));
+    const size_t tb = scan_bytes_ - (size_t)(t2 - (char*)scan_tmp_.p);
+    k_chunk_rest_count<W><<<grid_for(S.nactw, L::TILE, grid), kBlock, 0, s>>>(
+        actw_[0].as<int32_t>(), S.nactw, g_.rowptr, R, acc_[S.ac].as<uint64_t>(), alive,
+        sm.gmask, snap, cnt);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    inclusive_scan_i64(cnt, offs_.as<int64_t>(), S.nactw, t2, tb, s);
+    k_chunk_rest_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
+        actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, d + S.nactw);
+    MSBFS_HIP_CHECK(hipGetLastError());
+    launch_chunks(d + S.nactw, offs_.as<int64_t>() + S.nactw - 1, chunks_max - S.nactw);
+  } else if (S.nactw && !tiled) {
     if (pfx) {  // chunks of the row prefixes with ids < H only
       int64_t* cnt = scan_tmp_.as<int64_t>();
       char* t2 = (char*)scan_tmp_.p + (((size_t)S.nactw * sizeof(int64_t) + 255) & ~size_t(255));
@@ -418,33 +462,14 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                            scan_tmp_.p, scan_bytes_, s, kChunk);
     }
     const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
-    // Early exit across a vertex's chunks (coop) everywhere except on an explosive first
-    // bottom-up level (level 2: hardly any row gets covered, and round-robin chunk dealing
-    // balances the hubs better). When top-down ran longer (RMAT-30: first pull at level 3,
-    // most of every hub's groups already visited) the early exit skips most chunks.
-    const int coop = !first_bu || S.level != 2 ? 1 : 0;
     desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
     k_chunk_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
         actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, plen,
         desc_.as<ChunkDesc>());
     MSBFS_HIP_CHECK(hipGetLastError());
-    if (hub_lds) {
-      // exact chunk count = offs[nactw - 1], read on the device (no host round trip); one
-      // block per CU with the 128-KB hub bitmap (ids < 1M) except on the prefix level, whose
-      // prefixes end at the small one's bound (two blocks per CU)
-      const bool big = hub_big && !pfx;
-      auto ck = big ? k_bu_chunks<W, 256, 1024, kHubBig> : k_bu_chunks<W, 256, 1024, kHubW>;
-      ck<<<grid_for(chunks_max, 16, big ? 256 : 512), 1024, 0, s>>>(
-          desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive,
-          sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from,
-          coop, codes, code_from, snap, dprobe);
-    } else {
-      k_bu_chunks<W, 256, kBlock, 0><<<grid_for(chunks_max, kWaves, 8192), kBlock, 0, s>>>(
-          desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, g_.col, R, alive, sm.gmask,
-          acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(), filter_from, coop, codes, code_from,
-          snap, dprobe);
-    }
-    MSBFS_HIP_CHECK(hipGetLastError());
+    launch_chunks(desc_.as<ChunkDesc>(), offs_.as<int64_t>() + S.nactw - 1, chunks_max);
+  }
+  if (S.nactw && !tiled) {
     const int gw = grid_for(S.nactw, L::TILE, grid);
     k_bu_wide_finalize<W, COUNT, FUSE><<<gw, kBlock, 0, s>>>(
         actw_[0].as<int32_t>(), S.nactw, g_.rowptr, R, O, acc_[S.ac].as<uint64_t>(), alive,

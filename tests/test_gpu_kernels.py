@@ -69,6 +69,23 @@ def test_bitpar_direction_variants(msbfs_pkg, force_dir, wide):
         assert np.array_equal(r.edges, ref.edges)
 
 
+@pytest.mark.parametrize("wide", [2, 4, 16])
+def test_bitpar_two_pass_chunks(msbfs_pkg, wide):
+    """chunk2: the wide vertices of the early-exit pull levels pull their first chunk, then only
+    the open ones the rest (k_chunk_first / k_chunk_rest_count / k_chunk_rest_desc). Small
+    wide_degree thresholds put most vertices on the wide list (several chunks each with kChunk
+    = 1024 only for the hubs); exact F against the CPU oracle, with the lean pass forced on."""
+    m = msbfs_pkg
+    for name, g in _graphs(m)[:4] + [("rmat14", m.Graph.rmat(14, 16, 5))]:
+        qs = m.QuerySet.random(g.n, 300, 4, seed=wide)
+        ref = m.cpu_bfs(g, qs)
+        for tun in ({"chunk2": 1}, {"chunk2": 1, "lean_min": 0}):
+            with m.Solver(g.to_device(0), "bitpar", max_groups=qs.K, wide_degree=wide,
+                          tuning=tun) as s:
+                assert np.array_equal(s.run(qs).F, ref.F), (name, wide, tun)
+                assert np.array_equal(s.run(qs).F, ref.F), (name, wide, tun)
+
+
 @pytest.mark.parametrize("force_dir,wide", [(1, 64), (2, 64), (2, 2), (0, 8)])
 def test_dist_direction_variants(msbfs_pkg, force_dir, wide):
     m = msbfs_pkg
@@ -262,7 +279,7 @@ def test_bitpar_tiled_first_pull(msbfs_pkg, K):
             "td3": {"dirs": "TBT"}, "td3plain": {"dirs": "TBT", "tiles": 0},
             "pushbefore": {"push_after": 0}, "td3pushbefore": {"dirs": "TBT", "push_after": 0},
             "pushafter_nocodes": {"push_after": 1, "codes": 0}, "hskip": {"hskip": 1},
-            "hskip_nolean": {"hskip": 1, "lean_min": 1 << 40}}
+            "hskip_nolean": {"hskip": 1, "lean_min": 1 << 40}, "chunk2": {"chunk2": 1}}
     out = {}
     for name, tun in runs.items():
         with m.Solver(g, "bitpar", max_groups=qs.K, tuning=tun) as s:
