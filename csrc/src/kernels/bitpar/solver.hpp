@@ -105,6 +105,8 @@ struct Tuning {
   int hskip = 0;
   // two-pass chunk scheduling of the wide vertices on early-exit levels (k_chunk_first)
   int chunk2 = 0;
+  // one-lane-per-vertex pulls (W <= 2) refill a lane as soon as its vertex is done (k_bu_refill)
+  int refill = 0;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->

@@ -86,6 +86,26 @@ def test_bitpar_two_pass_chunks(msbfs_pkg, wide):
                 assert np.array_equal(s.run(qs).F, ref.F), (name, wide, tun)
 
 
+@pytest.mark.parametrize("K", [20, 64, 128])
+def test_bitpar_lane_refill(msbfs_pkg, K):
+    """refill: the one-lane-per-vertex pulls (1-2 words) hand a finished lane the next vertex of
+    its wave's slice (k_bu_refill); exact F against the CPU oracle on every test graph, with and
+    without the level-3 row skipping, with forced pull / push plans, and on a relabelled RMAT."""
+    m = msbfs_pkg
+    dg = m.DeviceGraph.rmat(15, 16, 5, device=0)
+    hg = dg.download()
+    dg.relabel_by_degree()
+    cases = [(name, g.to_device(0), g) for name, g in _graphs(m)] + [("rmat15r", dg, hg)]
+    for name, dev, host in cases:
+        qs = m.QuerySet.random(host.n, K, 5, seed=K + len(name))
+        ref = m.cpu_bfs(host, qs)
+        for tun in ({"refill": 1}, {"refill": 1, "dskip3": 0}, {"refill": 1, "dirs": "TBBBBBBB"},
+                    {"refill": 1, "dirs": "TBBTBBTB"}):
+            with m.Solver(dev, "bitpar", max_groups=K, tuning=tun) as s:
+                assert np.array_equal(s.run(qs).F, ref.F), (name, K, tun)
+                assert np.array_equal(s.run(qs).F, ref.F), (name, K, tun)
+
+
 @pytest.mark.parametrize("force_dir,wide", [(1, 64), (2, 64), (2, 2), (0, 8)])
 def test_dist_direction_variants(msbfs_pkg, force_dir, wide):
     m = msbfs_pkg

@@ -66,7 +66,7 @@ for s in "$@"; do
          for d in pmch1 pmch2 pmch3; do python tools/prof_summary.py gpurun_out/$d > gpurun_out/$d.md; done ;;
     pmcregex) # PMC_RE=<kernel regex>: three counter passes of one timed RMAT-26 step
          export TMPDIR=/tmp; R="${PMC_RE:-k_pfx_tiles}"; rm -rf gpurun_out/pmcr1 gpurun_out/pmcr2 gpurun_out/pmcr3
-         B="python bench.py --steps 1 --warmup 0 --verify 0"
+         B="${PMC_B:-python bench.py --steps 1 --warmup 0 --verify 0}"
          step pmcr1 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmcr1 -o run -- $B &&
          step pmcr2 300 rocprofv3 --pmc TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmcr2 -o run -- $B &&
          step pmcr3 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM --kernel-include-regex "$R" --output-format csv -d gpurun_out/pmcr3 -o run -- $B &&
