@@ -227,8 +227,8 @@ __device__ __forceinline__ void block_sum_add32(uint32_t val, uint32_t* dst, uin
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_push_tail_after(
     const int32_t* fl, int64_t nf, int32_t H, const int64_t* rowptr, const int32_t* col,
-    const uint64_t* R, const uint32_t* code, int32_t code_from, uint64_t* O,
-    const uint32_t* done, uint32_t* fbm, uint32_t* anyvis, Ctr* ctr, uint32_t* slabF) {
+    const uint64_t* R, const uint32_t* code, int32_t code_from, uint64_t* O, uint32_t* fbm,
+    uint32_t* anyvis, Ctr* ctr, uint32_t* slabF) {
   __shared__ uint32_t cnt[64 * W];
   __shared__ unsigned long long scratch[kWaves];
   __shared__ uint32_t scratch32[kWaves];
@@ -247,9 +247,8 @@ __global__ __launch_bounds__(kBlock) void k_push_tail_after(
     const int64_t b = rowptr[u], e = rowptr[u + 1];
     for (int64_t k = b + lane; k < e; k += 64) {
       const int32_t v = col[k];
-      // (a vertex done before this level has no output row written by the pull: skip it; one
-      // done during the level has every alive group already)
-      if (is_done(done, v)) continue;
+      // (every target has its output row: the tiles and the big vertices' finalize write one
+      // for the vertices done before this level too, holding every alive group)
       bool added = false;
       if (c != kDenseCode) {
         for (int s = 0; s < kCodeSlots; ++s) {
@@ -1118,8 +1117,11 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     if (valid) {
       v = wl[idx];
       if (fbm && is_done(done, v)) {
-        // (the tiled level's tail push also pushes into done vertices: leave their acc row clean)
-        stv<VW>(acc + (int64_t)v * W + slot * VW, vzero<VW>());
+        // (the tiled level's tail push also pushes into done vertices: leave their acc row clean;
+        // and give them their unchanged row in Wb, which k_push_tail_after filters against)
+        const int64_t vo = (int64_t)v * W + slot * VW;
+        stv<VW>(acc + vo, vzero<VW>());
+        stv<VW>(Wb + vo, ldv<VW>(R + vo));
         valid = false;
       }
     }

@@ -476,212 +476,6 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
 }
 
-// k_bu_full for one lane per vertex (W <= 2 words: hybrid phase C and round robin at 8 ranks,
-// RMAT-30's 32-group passes) with LANE REFILL (tuning key refill). A 64-vertex wave of
-// k_bu_full runs until its slowest vertex is covered: on RMAT-20/22 level 3 with 128 groups the
-// lanes are busy 71 % of the steps (tools/pull_steps_sim.py: mean 2.2 steps, the wave's
-// maximum 3.1). Here a lane that finishes takes the next vertex of its wave's contiguous list
-// slice at once. Every lane is a small pipeline, one round trip per iteration:
-//   list id (stage A) -> row offsets + own row (stage B) -> first column ids -> a step: the
-//   step's rows AND the next step's column ids -> ... -> finish (store, counters, flags, lists)
-// with the next vertex's id and offsets/row already loaded behind the current one. Loads are
-// gated by wave ballots with clamped addresses (no load under a divergent branch). No done
-// probes (dsnap) and no device-driven gate: the levels that need those keep k_bu_full.
-template <int W, int C1>
-__global__ __launch_bounds__(kBlock, W >= 2 ? 4 : 5) void k_bu_refill(
-    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
-    const uint64_t* R, uint64_t* Wb, int64_t n, const uint64_t* alive, const uint64_t* gmask,
-    uint32_t* done, int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* actw2,
-    int next_wide, uint32_t* slabF, int flags) {
-  using L = Lay<W>;
-  static_assert(L::G == 1, "one lane per vertex");
-  constexpr int VW = L::VW;
-  constexpr int CS = 4;  // rows per step (C1 > 0: the first step gathers C1)
-  static_assert(C1 >= 0 && C1 <= CS, "first step");
-  const bool skip = flags & kFlagSkipRows;
-  constexpr int QA = 768, QF = QA, QW = 128;
-  __shared__ int32_t qmem[kWaves][QA + QF + QW];
-  __shared__ unsigned long long scratch[kWaves];
-  __shared__ uint32_t wbase[kWaves + 1];
-  constexpr int CR = 65;
-  __shared__ uint32_t cnt[CR * W];
-  for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
-  __syncthreads();
-  const int wv = threadIdx.x >> 6;
-  int32_t* qa = qmem[wv];
-  int32_t* qf = qa + QA;
-  int32_t* qw = qf + QF;
-  uint32_t na = 0, nf = 0, nw = 0;  // (wave-uniform)
-  const RowBuf<W> rR = row_buf<W>(R, n), rO = row_buf<W>(Wb, n);
-  constexpr int voff = 0;
-  const int32_t zrow = (int32_t)n;
-  V<VW> am;
-#pragma unroll
-  for (int j = 0; j < VW; ++j) am.w[j] = alive[j] & gmask[j];
-  unsigned long long eu = 0, ef = 0, ev = 0;
-  BitCounter<VW, 5> bc;
-  bc.zero();
-  int nadd = 0;
-  // this wave's contiguous slice of the list (uniform)
-  const int64_t nwaves = (int64_t)gridDim.x * kWaves, wid = (int64_t)blockIdx.x * kWaves + wv;
-  int64_t cur = nact * wid / nwaves;
-  const int64_t lim = nact * (wid + 1) / nwaves;
-  // lane pipeline
-  int32_t qv = -1;                    // stage A: a list id
-  int32_t pv = -1;                    // stage B: id with offsets and own row loaded
-  int64_t pb = 0, pe = 0;
-  V<VW> pr = vzero<VW>();
-  int32_t v = -1;                     // the vertex being pulled
-  int64_t e = 0, end = 0, dcur = 0;   // next row position, row end, degree
-  int st = 0;                         // 1: column ids pending, 2: ids of the next step in u
-  bool first = false;                 // the next step is the vertex's first
-  V<VW> r = vzero<VW>(), unv = vzero<VW>(), acc = vzero<VW>();
-  int32_t u[CS];
-#pragma unroll
-  for (int c = 0; c < CS; ++c) u[c] = -1;
-  for (;;) {
-    // stage B (ids loaded last iteration -> offsets + own row)
-    {
-      const bool doB = qv >= 0 && pv < 0;
-      if (__ballot(doB)) {
-        const int32_t b = doB ? qv : 0;
-        const int64_t ob = rowptr[b], oe = rowptr[b + 1];
-        const V<VW> orow = ld_row<W, VW>(rR, doB ? qv : zrow, voff);
-        if (doB) {
-          pv = qv;
-          pb = ob;
-          pe = oe;
-          pr = orow;
-          qv = -1;
-        }
-      }
-    }
-    // refill: a free lane takes the loaded vertex
-    {
-      const bool take = v < 0 && pv >= 0;
-      if (take) {
-        v = pv;
-        e = pb;
-        end = pe;
-        dcur = pe - pb;
-        r = pr;
-        pv = -1;
-        st = 1;
-        first = true;
-#pragma unroll
-        for (int j = 0; j < VW; ++j) {
-          unv.w[j] = ~r.w[j] & am.w[j];
-          acc.w[j] = 0;
-        }
-      }
-    }
-    // stage A: free id slots take the next entries of the slice
-    {
-      const bool needA = qv < 0;
-      const uint64_t ma = __ballot(needA);
-      if (ma && cur < lim) {
-        const int64_t idx = cur + mbcnt64(ma);
-        const bool ok = needA && idx < lim;
-        const int32_t a = act[ok ? idx : cur];
-        if (ok) qv = a;
-        cur = min(cur + (int64_t)__popcll(ma), lim);
-      }
-    }
-    // a step: lanes with ids gather their rows; every pulling lane loads the next ids
-    const bool s2 = v >= 0 && st == 2;
-    const int len = first ? (C1 > 0 ? C1 : CS) : CS;  // (this step's rows)
-    V<VW> x[CS];
-#pragma unroll
-    for (int c = 0; c < CS; ++c) {
-      x[c] = vzero<VW>();
-      const bool need = s2 && c < len && u[c] >= 0;
-      if (__ballot(need)) x[c] = ld_row<W, VW>(rR, need ? u[c] : zrow, voff);
-    }
-    const int64_t ce = s2 ? e + len : e;  // ids of the next step (or of the first, st == 1)
-    int32_t un[CS];
-#pragma unroll
-    for (int c = 0; c < CS; ++c) {
-      const bool okc = v >= 0 && ce + c < end;
-      un[c] = -1;
-      if (__ballot(okc)) {
-        const int32_t t = col[okc ? ce + c : 0];
-        un[c] = okc ? t : -1;
-      }
-    }
-    bool open = false;
-    if (v >= 0) {
-#pragma unroll
-      for (int j = 0; j < VW; ++j) {
-#pragma unroll
-        for (int c = 0; c < CS; ++c) acc.w[j] |= x[c].w[j];
-        open |= (unv.w[j] & ~acc.w[j]) != 0;
-      }
-      if (s2) {
-        e += len;
-        first = false;
-      }
-      st = 2;
-#pragma unroll
-      for (int c = 0; c < CS; ++c) u[c] = un[c];
-    }
-    // finished: covered, or the row ran out
-    const bool fin = v >= 0 && (!open || (s2 && e >= end));
-    if (__ballot(fin)) {
-      V<VW> nwv = vzero<VW>();
-      bool anynew = false, notfull = false, rnz = false;
-      if (fin) {
-#pragma unroll
-        for (int j = 0; j < VW; ++j) {
-          nwv.w[j] = acc.w[j] & unv.w[j];
-          anynew |= nwv.w[j] != 0;
-          notfull |= (unv.w[j] & ~nwv.w[j]) != 0;
-          rnz |= r.w[j] != 0;
-        }
-        if (notfull || !skip) {
-          V<VW> nv;
-#pragma unroll
-          for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nwv.w[j];
-          st_row<W, VW>(rO, v, voff, nv);
-        }
-      }
-      bc.add(nwv);
-      if (++nadd == (1 << decltype(bc)::D) - 1) {
-        bc.template spill_strided32<CR>(cnt, 0);
-        nadd = 0;
-      }
-      const int64_t dv = fin ? dcur : 0;
-      wave_set_bits<true>(done, v, fin && !notfull);
-      const bool keep = fin && notfull, app = fin && anynew;
-      if (keep) eu += (unsigned long long)dv;
-      if (app) ef += (unsigned long long)dv;
-      const bool fst = app && !rnz;
-      wave_set_bits<true>(anyvis, v, fst);
-      if (fst) ev += (unsigned long long)dv;
-      wq_push(qa, na, keep && dv <= next_wide, v);
-      wq_push(qw, nw, keep && dv > next_wide, v);
-      wq_push(qf, nf, app, v);
-      if (na + 64 > QA) wq_flush(qa, na, act2, &ctr->act2.v);
-      if (nw + 64 > QW) wq_flush(qw, nw, actw2, &ctr->actw2.v);
-      if (nf + 64 > QF) wq_flush(qf, nf, fl2, &ctr->fl2.v);
-      if (fin) {
-        v = -1;
-        st = 0;
-      }
-    }
-    if (cur >= lim && !__ballot(v >= 0 || pv >= 0 || qv >= 0)) break;
-  }
-  wq_flush_block(qa, na, act2, &ctr->act2.v, wbase);
-  wq_flush_block(qw, nw, actw2, &ctr->actw2.v, wbase);
-  wq_flush_block(qf, nf, fl2, &ctr->fl2.v, wbase);
-  block_sum_add(eu, &ctr->eu2.v, scratch);
-  block_sum_add(ef, &ctr->ef2.v, scratch);
-  block_sum_add(ev, &ctr->ev2.v, scratch);
-  bc.template spill_strided32<CR>(cnt, 0);
-  __syncthreads();
-  uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
-  for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
-}
-
 // The lean first-row pass (k_bu_first's job, tuning key first_u = U > 0) with U tiles per wave
 // and iteration. k_bu_first's loop is one chain of four dependent loads per tile (list entry ->
 // first neighbour id -> done probe -> neighbour row; RMAT-26 level 4: 24.8M vertices, 1.6 ms, the

@@ -314,6 +314,10 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
         // (anyvis bits of this tile's vertices change only in this epilogue, after the read)
         const bool visl = lane < nv && ((swl >> (vlane & 31)) & 1u);
         const uint64_t bok = __ballot(okl), bvis = __ballot(visl);
+        // !ACC: vertices done before the level get their (unchanged) row in O as well, so the
+        // tail push after the tiles needs no done probe (their rows already hold every alive
+        // group: its plain-load filter skips them)
+        const uint64_t bput = ACC ? bok : __ballot(lane < nv && degl > 0);
         uint32_t m_done = 0, m_new = 0, m_first = 0;
         // two passes per batch: own rows and pushed rows of 16 vertices in flight
         constexpr int NH = 1;
@@ -340,9 +344,10 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           const int32_t v = v0 + i * nparts;
           const bool valid = (bok >> i) & 1ull;
           const uint32_t deg = (uint32_t)__shfl((int)degl, i);
+          const bool put = (bput >> i) & 1ull;  // (valid, or done with edges when !ACC)
           V<VW> r = vzero<VW>(), a = vzero<VW>();
+          if (put) r = rr[k];
           if (valid) {
-            r = rr[k];
 #pragma unroll
             for (int j = 0; j < VW; ++j) a.w[j] = y[i * W + slot * VW + j] | pa[k].w[j];
           }
@@ -363,7 +368,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
             notfull |= (unv & ~nw.w[j]) != 0;
             rnz |= r.w[j] != 0;
           }
-          if (valid) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
+          if (put) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
           bc.add(nw);
           if (++nadd == (1 << decltype(bc)::D) - 1) {
             bc.template spill_strided32<CR>(cnt, slot);

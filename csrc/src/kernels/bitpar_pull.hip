@@ -290,8 +290,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       if (rows + gp > 3 * kMaxGrid) fail("tail push: counter slab rows exhausted");
       k_push_tail_after<W><<<gp, kBlock, 0, s>>>(
           fl_[S.fc].as<int32_t>(), S.nf, kPfxH, g_.rowptr, g_.col, R, codes, code_from, O,
-          done_.as<uint32_t>(), fbm_tile_.as<uint32_t>(), anyvis_.as<uint32_t>(), ctr_.as<Ctr>(),
-          slabF<W>(rows));
+          fbm_tile_.as<uint32_t>(), anyvis_.as<uint32_t>(), ctr_.as<Ctr>(), slabF<W>(rows));
       MSBFS_HIP_CHECK(hipGetLastError());
       rows += gp;
       S.push_after = false;
@@ -378,16 +377,6 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
               &ctr_.as<Ctr>()->touched.v, nullptr, BuGate{});
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gn;
-      } else if (FUSE && !filt && tun_.full && W <= 2 && tun_.refill && !dprobe) {
-        if constexpr (W <= 2) {  // one lane per vertex, lanes refilled (see k_bu_refill)
-          auto kr = short1 ? k_bu_refill<W, 1> : k_bu_refill<W, 0>;
-          kr<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n,
-                                   alive, sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
-                                   fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
-                                   anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
-                                   slabF<W>(rows), (skip3 ? kFlagSkipRows : 0));
-          rows += gn;
-        }
       } else if (FUSE && !filt && tun_.full) {
         auto kf = short1 ? k_bu_full<W, full_cs<W>(), 1> : k_bu_full<W, full_cs<W>(), 0>;
         kf<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive,

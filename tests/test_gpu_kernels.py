@@ -79,31 +79,11 @@ def test_bitpar_two_pass_chunks(msbfs_pkg, wide):
     for name, g in _graphs(m)[:4] + [("rmat14", m.Graph.rmat(14, 16, 5))]:
         qs = m.QuerySet.random(g.n, 300, 4, seed=wide)
         ref = m.cpu_bfs(g, qs)
-        for tun in ({"chunk2": 1}, {"chunk2": 1, "lean_min": 0}):
+        for tun in ({"chunk2": 1}, {"chunk2": 1, "lean_min": 0}, {"chunk2": 0}):
             with m.Solver(g.to_device(0), "bitpar", max_groups=qs.K, wide_degree=wide,
                           tuning=tun) as s:
                 assert np.array_equal(s.run(qs).F, ref.F), (name, wide, tun)
                 assert np.array_equal(s.run(qs).F, ref.F), (name, wide, tun)
-
-
-@pytest.mark.parametrize("K", [20, 64, 128])
-def test_bitpar_lane_refill(msbfs_pkg, K):
-    """refill: the one-lane-per-vertex pulls (1-2 words) hand a finished lane the next vertex of
-    its wave's slice (k_bu_refill); exact F against the CPU oracle on every test graph, with and
-    without the level-3 row skipping, with forced pull / push plans, and on a relabelled RMAT."""
-    m = msbfs_pkg
-    dg = m.DeviceGraph.rmat(15, 16, 5, device=0)
-    hg = dg.download()
-    dg.relabel_by_degree()
-    cases = [(name, g.to_device(0), g) for name, g in _graphs(m)] + [("rmat15r", dg, hg)]
-    for name, dev, host in cases:
-        qs = m.QuerySet.random(host.n, K, 5, seed=K + len(name))
-        ref = m.cpu_bfs(host, qs)
-        for tun in ({"refill": 1}, {"refill": 1, "dskip3": 0}, {"refill": 1, "dirs": "TBBBBBBB"},
-                    {"refill": 1, "dirs": "TBBTBBTB"}):
-            with m.Solver(dev, "bitpar", max_groups=K, tuning=tun) as s:
-                assert np.array_equal(s.run(qs).F, ref.F), (name, K, tun)
-                assert np.array_equal(s.run(qs).F, ref.F), (name, K, tun)
 
 
 @pytest.mark.parametrize("force_dir,wide", [(1, 64), (2, 64), (2, 2), (0, 8)])
@@ -313,6 +293,31 @@ def test_bitpar_tiled_first_pull(msbfs_pkg, K):
     sub = qs.subset(np.arange(0, K, 97))
     with m.Solver(g, "dist") as ds:
         assert np.array_equal(ds.run(sub).F, out["tiles"][::97])
+    g.close()
+
+
+def test_bitpar_tiled_done_before_pull(msbfs_pkg):
+    """Every group holds the top hub: all of its neighbours are visited by every group at level
+    1, so they are done before the tiled level 2 (the tile epilogue and the big vertices'
+    finalize still write their rows for the tail push after the tiles, which filters against
+    them instead of probing the done bitmap). Same F with the push after / before the tiles and
+    without tiles."""
+    m = msbfs_pkg
+    g = m.DeviceGraph.rmat(23, 16, 11, device=0)
+    g.relabel_by_degree()
+    top = int(np.nonzero(g.relabel_map() == 0)[0][0])  # user id of internal id 0
+    base = m.QuerySet.random(g.n, 520, 6, seed=3)
+    qs = m.QuerySet.from_groups([list(x) + [top] for x in base.groups()])
+    out = {}
+    for name, tun in {"after": {}, "before": {"push_after": 0}, "plain": {"tiles": 0}}.items():
+        with m.Solver(g, "bitpar", max_groups=qs.K, tuning=tun) as s:
+            s.prepare()
+            out[name] = s.run(qs).F
+            assert np.array_equal(s.run(qs).F, out[name]), name
+    assert np.array_equal(out["after"], out["plain"])
+    assert np.array_equal(out["before"], out["plain"])
+    with m.Solver(g, "dist") as ds:
+        assert np.array_equal(ds.run(qs.subset(np.arange(0, qs.K, 101))).F, out["plain"][::101])
     g.close()
 
 
