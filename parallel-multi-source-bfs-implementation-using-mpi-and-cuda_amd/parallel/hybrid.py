@@ -351,7 +351,8 @@ def overlapped_exchange_ms(phase_a_ms: float, ready_ms, piece_bytes, gbps: float
 
 
 def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
-                  coded: Optional[bool] = None, chunks: int = 1) -> np.ndarray:
+                  coded: Optional[bool] = None, chunks: int = 1,
+                  wbeg: Optional[np.ndarray] = None) -> np.ndarray:
     """Run the hybrid algorithm for `world` ranks sequentially in ONE process on one GPU (no
     torch.distributed): phase A of every rank, a host-side all-to-all, phase C of every rank.
     Returns the full F vector. Used by the GPU tests and to time per-rank phases: with
@@ -359,14 +360,19 @@ def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
     send/recv bytes). coded: zero-word coded exchange (default: coding_default()), decoded on the
     GPU. chunks > 1 (dense only): phase A runs chunked like the overlapped exchange of
     HybridRunner; each piece's ready time (CUDA events after its pack) and bytes are recorded
-    ("pieces") so that tools/hybrid_sim.py can price only the exchange phase A does not hide."""
+    ("pieces") so that tools/hybrid_sim.py can price only the exchange phase A does not hide.
+    wbeg: a custom word split (world + 1 non-decreasing entries from 0 to ceil(K/64); default
+    word_split, the even one)."""
     import torch
 
     coded = coding_default() if coded is None else bool(coded)
     K = queries.K
     g = solver.graph
     n_eff = g.hybrid_extent()
-    wbeg = word_split(K, world)
+    wt = (K + 63) // 64
+    wbeg = word_split(K, world) if wbeg is None else np.asarray(wbeg, dtype=np.int32)
+    if len(wbeg) != world + 1 or wbeg[0] != 0 or wbeg[-1] != wt or np.any(np.diff(wbeg) < 0):
+        raise ValueError("wbeg: world + 1 non-decreasing word bounds from 0 to ceil(K/64)")
     dev = torch.device("cuda", g.device)
     sends, outs, lens = [], [], []
     chunks = 1 if coded else max(1, int(chunks))

@@ -233,6 +233,27 @@ def test_hybrid_matches_solver_rmat(msbfs_pkg, world, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wbeg", [[0, 3, 5, 7, 9, 11, 13, 15, 16], [0, 1, 1, 8, 9, 12, 14, 15, 16],
+                                  [0, 0, 16, 16, 16, 16, 16, 16, 16]])
+def test_hybrid_uneven_word_split(msbfs_pkg, wbeg):
+    """Uneven word splits (tools/hybrid_balance.py 'uneven': fewer words for the rank with the
+    latest groups), including ranks that own no word: every rank still runs phase A over its
+    vertices and exchanges, the F is the solver's (dense and coded exchange, chunked pieces)."""
+    m = msbfs_pkg
+    H = _H()
+    dg = m.DeviceGraph.rmat(14, 16, 3, device=0, relabel=True)
+    qs = m.QuerySet.random(dg.n, 1024, 16, seed=41)
+    with m.Solver(dg, "bitpar", max_groups=1024) as s:
+        ref = s.run(qs).F
+        wb = np.array(wbeg, dtype=np.int32)
+        assert np.array_equal(H.emulate_ranks(s, qs, 8, wbeg=wb), ref)
+        assert np.array_equal(H.emulate_ranks(s, qs, 8, wbeg=wb, coded=True), ref)
+        assert np.array_equal(H.emulate_ranks(s, qs, 8, wbeg=wb, chunks=4), ref)
+        with pytest.raises(ValueError):
+            H.emulate_ranks(s, qs, 8, wbeg=wb[:-1])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world,K", [(8, 1024), (3, 700), (2, 5)])
 def test_hybrid_coded_send_matches_numpy_codec(msbfs_pkg, world, K):
     """k_code_bits/k_code_emit vs encode_np of the dense phase-A send segments, and the GPU

@@ -12,6 +12,9 @@ prints every rank's phase C for each ordering:
   snake    groups sorted by a lateness key, dealt to the ranks in snake order (balanced mix)
   cluster  the same sorted order, contiguous (late groups together)
   pair     sorted order, the last rank holding the 64 latest and the 64 earliest groups
+  uneven   the cluster order with an uneven word split (--uneven, default 3,2,2,2,2,2,2,1 words
+           for 8 ranks: fewer groups for the rank that holds the latest ones; it also receives
+           less of the exchange, the earliest rank more)
 
 Lateness key of a group = the smallest internal (degree-descending) id among its sources, i.e.
 the degree rank of its best-connected source: a group whose every source has low degree reaches
@@ -54,6 +57,8 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--orders", nargs="+", default=None, help="subset of the orderings to run")
+    ap.add_argument("--uneven", default="3,2,2,2,2,2,2,1",
+                    help="words per rank of the uneven split (sum = ceil(K/64))")
     args = ap.parse_args()
 
     import msbfs
@@ -69,7 +74,10 @@ def main():
     rng = np.random.default_rng(1)
     plans = {"orig": np.arange(K), "shuffle1": rng.permutation(K), "shuffle2": rng.permutation(K),
              "snake": snake(order, K, N, wbeg), "cluster": order,
-             "pair": np.concatenate([order[64:K - 64], order[:64], order[K - 64:]])}
+             "pair": np.concatenate([order[64:K - 64], order[:64], order[K - 64:]]),
+             "uneven": order}
+    words = [int(x) for x in args.uneven.split(",")]
+    wb_uneven = np.concatenate([[0], np.cumsum(words)]).astype(np.int32)
     with msbfs.Solver(g, "bitpar", max_groups=K) as s:
         ref = s.run(qs)
         H.emulate_ranks(s, qs, N)  # warm
@@ -78,18 +86,21 @@ def main():
                 continue
             sub = qs.subset(perm)
             best = None
+            wb = wb_uneven if name == "uneven" else wbeg
             for _ in range(args.reps):
                 tim = []
-                F = H.emulate_ranks(s, sub, N, timings=tim)
+                F = H.emulate_ranks(s, sub, N, timings=tim, wbeg=wb)
                 c = [x["phase_c_ms"] for x in tim]
                 best = c if best is None else [min(a, b) for a, b in zip(best, c)]
             ok = bool(np.array_equal(F, ref.F[perm]))
-            keys = [int(np.median(key[perm[64 * int(wbeg[r]):64 * int(wbeg[r + 1])]]))
-                    for r in range(N)]
+            keys = [int(np.median(key[perm[64 * int(wb[r]):64 * int(wb[r + 1])]]))
+                    if wb[r + 1] > wb[r] else -1 for r in range(N)]
             print(json.dumps({"order": name, "correct": ok, "phase_c_max": round(max(best), 3),
                               "phase_c_mean": round(float(np.mean(best)), 3),
                               "phase_c": [round(x, 3) for x in best],
                               "levels_c": [x["levels_c"] for x in tim],
+                              "words": [int(wb[r + 1] - wb[r]) for r in range(N)],
+                              "recv_MB": [round(x["recv_bytes"] / 2**20, 1) for x in tim],
                               "median_key": keys}), flush=True)
     g.close()
 
