@@ -48,7 +48,7 @@ struct Args {
   int spmd = 0;
   int max_words = 0;    // bit-parallel: at most 64*max_words groups per solver pass (0: all fit)
   int async_slots = 0;  // asynchronous MIN slots before a drain (0: Comm::kAsyncSlots; tests)
-  int chunks = 0;       // hybrid: pieces of the overlapped exchange (0: 4 with RCCL, else 1)
+  int chunks = 0;       // hybrid: pieces of the overlapped exchange (0: 8 with RCCL, else 1)
   bool cache = false, json = false, sort_rows = false, relabel = true;
   bool host_csr = false;  // build the CSR of a graph file on the host (default: on the device)
 };
@@ -380,7 +380,7 @@ int rank_main(Args a, std::unique_ptr<Comm> world, bool upgraded) {
     // communicator's stream). Every rank's range bounds are agreed on here (one SUM all-reduce).
     const int nchunks = (hybrid && !hcoded)
                             ? std::max(1, std::min(a.chunks > 0 ? a.chunks
-                                                                : (comm->device_collectives() ? 4 : 1),
+                                                                : (comm->device_collectives() ? 8 : 1),
                                                    256))
                             : 1;
     std::vector<int64_t> cbounds;  // [P][nchunks + 1]
