@@ -118,10 +118,13 @@ void device_graph_sort_rows(DeviceGraph& g, hipStream_t s);
 void device_graph_relabel_by_degree(DeviceGraph& g, hipStream_t s);
 
 // ---- solvers ---------------------------------------------------------------------------------
+constexpr int kDefaultWideDegree = 32;
 struct SolverOptions {
   double alpha = 14.0;  // top-down -> bottom-up when frontier edges > unexplored edges / alpha
   double beta = 24.0;   // bottom-up -> top-down when frontier vertices < active vertices / beta
-  int wide_degree = 32; // first bottom-up level: vertices above this degree go to the chunk kernel
+  // first bottom-up level: vertices above this degree go to the chunk kernel (at the default,
+  // bit-parallel passes of <= 4 words use the tuning key wide_few instead)
+  int wide_degree = kDefaultWideDegree;
   int force_dir = 0;    // 0 auto, 1 top-down only, 2 bottom-up after level 0
   int max_words = 16;   // bit-parallel: at most 64*max_words groups per batch
   bool count_edges = false;

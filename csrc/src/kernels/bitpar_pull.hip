@@ -183,7 +183,10 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   if (!S.have_active && !tiled) {
     // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
     // off only for much higher degrees, so later lists are split at a higher threshold
-    const int wide0 = S.bu_levels == 0 ? opt.wide_degree : next_wide;
+    const int wide0 = S.bu_levels != 0 ? next_wide
+                      : (W <= 4 && tun_.wide_few > 0 && opt.wide_degree == kDefaultWideDegree)
+                          ? tun_.wide_few
+                          : opt.wide_degree;
     k_build_active<4096><<<grid_for(S.cnt, 4096, INT32_MAX), kBlock, 0, s>>>(
         S.cnt, S.part, S.nparts, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
         actw_[0].as<int32_t>(), ctr_.as<Ctr>());

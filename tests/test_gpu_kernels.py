@@ -86,6 +86,20 @@ def test_bitpar_two_pass_chunks(msbfs_pkg, wide):
                 assert np.array_equal(s.run(qs).F, ref.F), (name, wide, tun)
 
 
+@pytest.mark.parametrize("wide_few", [0, 8, 128, 1 << 20])
+def test_bitpar_first_pull_wide_threshold(msbfs_pkg, wide_few):
+    """wide_few: the first pull level's wide threshold for passes of <= 4 words (while
+    wide_degree is at its default); 0 keeps wide_degree. Exact F for 1, 2 and 4 words."""
+    m = msbfs_pkg
+    for name, g in _graphs(m)[:4] + [("rmat14", m.Graph.rmat(14, 16, 5))]:
+        for K in (40, 100, 250):
+            qs = m.QuerySet.random(g.n, K, 6, seed=K)
+            ref = m.cpu_bfs(g, qs)
+            with m.Solver(g.to_device(0), "bitpar", max_groups=K,
+                          tuning={"wide_few": wide_few}) as s:
+                assert np.array_equal(s.run(qs).F, ref.F), (name, K, wide_few)
+
+
 @pytest.mark.parametrize("force_dir,wide", [(1, 64), (2, 64), (2, 2), (0, 8)])
 def test_dist_direction_variants(msbfs_pkg, force_dir, wide):
     m = msbfs_pkg
