@@ -78,6 +78,7 @@ struct Tuning {
   // hold at most bu_max vertices (0 = host-driven pull levels; needs batch > 1)
   int64_t bu_max = 1 << 20;
   int tiles = 1;       // first pull level over static vertex tiles (bitpar/tiles.hpp)
+  int tiles_w = 8;     // fewest words per vertex that take the tiled first pull level (4, 8 or 16)
   // unfiltered pull levels (the second pull level on, lean overflow, device-driven batches) run
   // k_bu_full (structured-buffer rows, wave-private list queues; bitpar/pull_full.hpp) instead
   // of k_bu_narrow

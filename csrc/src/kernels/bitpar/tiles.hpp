@@ -34,6 +34,13 @@
 #include "common.hpp"
 #include "pull.hpp"
 
+#ifndef TILE_SLICES
+#define TILE_SLICES 5
+#endif
+#ifndef TILE_NH
+#define TILE_NH 1
+#endif
+
 namespace msbfs {
 namespace bp {
 
@@ -167,8 +174,6 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
   __shared__ unsigned long long Y[NWV][YW];
   __shared__ uint32_t lst[NWV][kRound];
   __shared__ uint32_t cnt[CR * W];
-  __shared__ unsigned long long scratch[NWV];
-  __shared__ uint32_t scratch32[NWV];
   for (int i = threadIdx.x; i < kTileHubW; i += kTileBlock) hub[i] = pvis[i];
   for (int i = threadIdx.x; i < CR * W; i += kTileBlock) cnt[i] = 0;
   __syncthreads();
@@ -180,11 +185,18 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
   __shared__ unsigned long long amask[W];
   if (threadIdx.x < W) amask[threadIdx.x] = alive[threadIdx.x] & gmask[threadIdx.x];
   __syncthreads();
-  unsigned long long ef = 0, ev = 0;
-  uint32_t nfc = 0;
+  // frontier count and degree sums per wave in LDS, added per tile from the tile masks (no
+  // 64-bit per-lane accumulators live through the round loop: registers for the pipeline)
+  __shared__ unsigned long long wef[NWV], wev[NWV];
+  __shared__ uint32_t wnf[NWV];
+  if (threadIdx.x < NWV) {
+    wef[threadIdx.x] = 0;
+    wev[threadIdx.x] = 0;
+    wnf[threadIdx.x] = 0;
+  }
   // 5 slices: a spill (one LDS add per set counter bit, ~100 per lane at level 2) every 31
   // passes (6 slices do not fit the 128 VGPRs of a 1024-thread block at 16 words)
-  BitCounter<VW, 5> bc;
+  BitCounter<VW, TILE_SLICES> bc;
   bc.zero();
   int nadd = 0;
   const int64_t nwaves = (int64_t)gridDim.x * NWV;
@@ -320,7 +332,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
         const uint64_t bput = ACC ? bok : __ballot(lane < nv && degl > 0);
         uint32_t m_done = 0, m_new = 0, m_first = 0;
         // two passes per batch: own rows and pushed rows of 16 vertices in flight
-        constexpr int NH = 1;
+        constexpr int NH = TILE_NH;
 #pragma unroll
         for (int h = 0; h < NP; h += NH) {
           if (h * VPW >= nv) break;
@@ -343,7 +355,6 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           const int i = p + sub;
           const int32_t v = v0 + i * nparts;
           const bool valid = (bok >> i) & 1ull;
-          const uint32_t deg = (uint32_t)__shfl((int)degl, i);
           const bool put = (bput >> i) & 1ull;  // (valid, or done with edges when !ACC)
           V<VW> r = vzero<VW>(), a = vzero<VW>();
           if (put) r = rr[k];
@@ -383,15 +394,12 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
           m_done |= (gval & ~gnf) << p;
           m_new |= gnew << p;
           m_first |= gfirst << p;
-          const bool g_new = (gnew >> sub) & 1u, g_first = (gfirst >> sub) & 1u;
-          const bool leader = valid && slot == 0;
-          if (leader && g_new) {
-            ++nfc;
-            ef += deg;
-          }
-          if (leader && g_first) ev += deg;
         }
         }
+        // (bit i of the masks = vertex i = lane i's degree; m_new / m_first hold valid vertices)
+        if ((m_new >> lane) & 1u) atomicAdd(&wef[wv], (unsigned long long)degl);
+        if ((m_first >> lane) & 1u) atomicAdd(&wev[wv], (unsigned long long)degl);
+        if (lane == 0) wnf[wv] += (uint32_t)__popc(m_new);
         if (nparts == 1) {
           if (lane == 0) {
             tile_mask_or(done, v0, m_done);
@@ -412,11 +420,20 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
 #pragma unroll
     for (int q = 0; q < Q; ++q) pkc[q] = pkb[q];
   }
-  block_sum_add32(nfc, &ctr->fl2.v, scratch32);
-  block_sum_add(ef, &ctr->ef2.v, scratch);
-  block_sum_add(ev, &ctr->ev2.v, scratch);
   bc.template spill_strided32<CR>(cnt, slot);
   __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    unsigned long long b = 0, c = 0;
+    for (int w = 0; w < NWV; ++w) {
+      a += wnf[w];
+      b += wef[w];
+      c += wev[w];
+    }
+    if (a) atomicAdd(&ctr->fl2.v, a);
+    if (b) atomicAdd(&ctr->ef2.v, b);
+    if (c) atomicAdd(&ctr->ev2.v, c);
+  }
   uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
   for (int i = threadIdx.x; i < 64 * W; i += kTileBlock) row[i] = cnt[i + (i >> 6)];
 }

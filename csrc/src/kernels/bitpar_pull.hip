@@ -174,7 +174,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   // the first pull level at level 2 with the prefix pull streams static vertex tiles
   // (bitpar/tiles.hpp) instead of pulling per vertex from active lists
   constexpr int kHubW = 14336, kHubBig = 32768;
-  const bool tiled = !COUNT && W >= 8 && tun_.tiles && tun_.pfx == 2 && S.bu_levels == 0 &&
+  const bool tiled = !COUNT && W >= 4 && W >= tun_.tiles_w && tun_.tiles && tun_.pfx == 2 && S.bu_levels == 0 &&
                      S.level == 2 && g_.rows_sorted && n <= INT32_MAX &&
                      n > (int64_t)kHubBig * 32 * 4 &&
                      ((S.lazy && S.bu_levels == 0) || (double)S.ev < kFilterFrac * (double)g_.nnz) &&

@@ -50,6 +50,10 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "hskip") hskip = (int)to_num(key, v);
   else if (key == "chunk2") chunk2 = (int)to_num(key, v);
   else if (key == "wide_few") wide_few = (int)to_num(key, v);
+  else if (key == "tiles_w") {
+    tiles_w = (int)to_num(key, v);
+    if (tiles_w != 4 && tiles_w != 8 && tiles_w != 16) fail("tuning: tiles_w must be 4, 8 or 16");
+  }
   else if (key == "first_u") {
     first_u = (int)to_num(key, v);
     if (first_u != 0 && first_u != 2 && first_u != 4) fail("tuning: first_u must be 0, 2 or 4");
@@ -59,7 +63,7 @@ void Tuning::set(const std::string& key, const std::string& v) {
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip first_u push_after dskip3 hskip chunk2 wide_few dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip first_u push_after dskip3 hskip chunk2 wide_few tiles_w dirs)");
   }
 }
 

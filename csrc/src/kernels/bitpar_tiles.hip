@@ -63,7 +63,7 @@ const BitparSolver::TileSet* BitparSolver::pfx_tiles(int W, int part, int nparts
   if (!tiles_ok_ || !tun_.tiles) return nullptr;
   // (4 words: no sparse codes, every visited hub's row gathered: RMAT-26 / 256 groups ran
   // level 2 in 9.7 ms tiled vs 7.4 ms per vertex)
-  if (W < 8) return nullptr;
+  if (W < 4 || W < tun_.tiles_w) return nullptr;
   for (auto it = tilesets_.begin(); it != tilesets_.end();) {
     TileSet& T = **it;
     if (T.key[0] != (const void*)g_.rowptr || T.key[1] != (const void*)g_.col) {
@@ -189,8 +189,8 @@ template <int W>
 int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t* O,
                              const uint32_t* snap, const uint32_t* codes, int32_t code_from,
                              int rows) {
-  if constexpr (W < 8) {
-    fail("tiled pull: needs 8 or more words");
+  if constexpr (W < 4) {
+    fail("tiled pull: needs 4 or more words");
   } else {
   const TileSet* T = pfx_tiles(W, S.part, S.nparts, s);
   const Small sm = small();

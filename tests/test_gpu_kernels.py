@@ -293,7 +293,10 @@ def test_bitpar_tiled_first_pull(msbfs_pkg, K):
             "td3": {"dirs": "TBT"}, "td3plain": {"dirs": "TBT", "tiles": 0},
             "pushbefore": {"push_after": 0}, "td3pushbefore": {"dirs": "TBT", "push_after": 0},
             "pushafter_nocodes": {"push_after": 1, "codes": 0}, "hskip": {"hskip": 1},
-            "hskip_nolean": {"hskip": 1, "lean_min": 1 << 40}, "chunk2": {"chunk2": 1}}
+            "hskip_nolean": {"hskip": 1, "lean_min": 1 << 40}, "chunk2": {"chunk2": 1},
+            # tiles from 4 words on (K = 200: W = 4, no codes there)
+            "tiles4": {"tiles_w": 4}, "tiles4_pushbefore": {"tiles_w": 4, "push_after": 0},
+            "td3tiles4": {"dirs": "TBT", "tiles_w": 4}}
     out = {}
     for name, tun in runs.items():
         with m.Solver(g, "bitpar", max_groups=qs.K, tuning=tun) as s:
