@@ -19,6 +19,8 @@
 //          hybrid-coded: the same with the zero-word coded all-to-all)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <chrono>
 #include <climits>
 #include <cstdio>
@@ -664,6 +666,16 @@ int main(int argc, char* argv[]) {
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) fail("no GPU visible (use --algo cpu)");
         std::vector<int> devs(a.spmd);
         for (int r = 0; r < a.spmd; ++r) devs[r] = (r % a.numGPU) % ndev;
+        {
+          std::vector<int> sd(devs);
+          std::sort(sd.begin(), sd.end());
+          const bool dup = std::adjacent_find(sd.begin(), sd.end()) != sd.end();
+          if (dup && a.comm == "rccl")
+            fail("--comm rccl needs one GPU per --spmd rank (RCCL rejects repeated devices); "
+                 "lower --spmd or use --comm auto / host");
+          if (dup)
+            fprintf(stderr, "msbfs: --spmd %d shares GPUs: host collectives (no RCCL)\n", a.spmd);
+        }
         comms = upgrade_thread_comms_rccl(std::move(comms), devs);
         // (as maybe_upgrade_rccl: RCCL needs one rank per GPU; never a silent fallback)
         if (a.comm == "rccl" && comms[0]->name() != "rccl")

@@ -350,7 +350,7 @@ class BitparSolver final : public Solver {
   DevBuf vis_[2], acc_[2], stamp_, done_, act_[2], actw_[2], fl_[2], touched_, offs_, scan_tmp_,
       ctr_, small_, pairs_, slabF_, slabE_, anyvis_, desc_;
   size_t scan_bytes_ = 0;
-  std::unique_ptr<PinnedBuf> hctr_, hsmall_;
+  std::unique_ptr<PinnedBuf> hctr_, hsmall_, hsrc_;  // (hsrc_: start_batch's H2D staging)
   int32_t epoch_ = 0;
   int64_t n_eff_ = 0;
   const void* eff_key_[3] = {nullptr, nullptr, nullptr};

@@ -227,16 +227,20 @@ void BitparSolver::phase_c_impl(int64_t K, int w_begin, int w_count, int nparts,
   MSBFS_HIP_CHECK(hipMemsetAsync(small_.p, 0, small_.bytes, s));
   const Small sm = small();
   {
-    uint64_t ha[2][16] = {{0}};  // alive, gmask
+    // alive, gmask (pinned staging, as start_batch: a pageable copy now and then stalled ms)
+    if (!hsrc_ || hsrc_->bytes < 32 * sizeof(uint64_t))
+      hsrc_ = std::make_unique<PinnedBuf>(32 * sizeof(uint64_t));
+    uint64_t* ha = hsrc_->as<uint64_t>();
+    std::fill(ha, ha + 32, 0ull);
     for (int w = 0; w < w_count; ++w)
       for (int b = 0; b < 64; ++b) {
         const int64_t k = (int64_t)(w_begin + w) * 64 + b;
         if (k >= K) break;
-        ha[1][w] |= 1ull << b;
-        if (reduced[K + k] > 0) ha[0][w] |= 1ull << b;
+        ha[16 + w] |= 1ull << b;
+        if (reduced[K + k] > 0) ha[w] |= 1ull << b;
       }
-    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[0], ha[0], sizeof(ha[0]), hipMemcpyHostToDevice, s));
-    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, ha[1], sizeof(ha[1]), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[0], ha, 16 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, ha + 16, 16 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     MSBFS_HIP_CHECK(hipStreamSynchronize(s));
   }
   if (n_eff > 0) {  // vertices >= n_eff have no edges: no kernel reads their rows or bits

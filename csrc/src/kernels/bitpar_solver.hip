@@ -204,23 +204,32 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
       }
     }
   const int64_t np = (int64_t)hp.size();
+  // the batch's masks and source pairs go up from one pinned staging buffer (pageable copies
+  // stage through the runtime and now and then stalled a step: RMAT-26 / 1024 groups, 1 step in
+  // ~10-30 took +6 ms outside the level loop, tools/step_split.py); the read_ctr below retires
+  // the copies before the buffer can be rewritten
+  const int64_t np1 = std::max<int64_t>(np, 1);
+  const size_t hbytes = 32 * sizeof(uint64_t) + (size_t)np1 * 2 * sizeof(int32_t);
+  if (!hsrc_ || hsrc_->bytes < hbytes) hsrc_ = std::make_unique<PinnedBuf>(hbytes + hbytes / 2);
   {
     // gmask = the batch's groups; alive = groups with at least one valid source (computed here:
     // an atomicOr per source pair onto 16 words serialised k_init, ~0.1 ms per batch)
-    uint64_t hm[2][16] = {{0}};
-    for (int64_t k = 0; k < nb; ++k) hm[0][k >> 6] |= 1ull << (k & 63);
-    for (int64_t i = 0; i < np; ++i) hm[1][hk[i] >> 6] |= 1ull << (hk[i] & 63);
-    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, hm[0], sizeof(hm[0]), hipMemcpyHostToDevice, s));
-    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[0], hm[1], sizeof(hm[1]), hipMemcpyHostToDevice, s));
-    MSBFS_HIP_CHECK(hipStreamSynchronize(s));  // hm is a stack buffer
+    uint64_t* hm = hsrc_->as<uint64_t>();
+    std::fill(hm, hm + 32, 0ull);
+    for (int64_t k = 0; k < nb; ++k) hm[k >> 6] |= 1ull << (k & 63);
+    for (int64_t i = 0; i < np; ++i) hm[16 + (hk[i] >> 6)] |= 1ull << (hk[i] & 63);
+    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, hm, 16 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[0], hm + 16, 16 * sizeof(uint64_t),
+                                   hipMemcpyHostToDevice, s));
   }
-  pairs_.ensure((size_t)std::max<int64_t>(np, 1) * 2 * sizeof(int32_t));
+  pairs_.ensure((size_t)np1 * 2 * sizeof(int32_t));
   int32_t* dpv = pairs_.as<int32_t>();
-  int32_t* dpk = dpv + std::max<int64_t>(np, 1);
-  hp.insert(hp.end(), hk.begin(), hk.end());
+  int32_t* dpk = dpv + np1;
   if (np) {
-    MSBFS_HIP_CHECK(hipMemcpyAsync(dpv, hp.data(), np * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    MSBFS_HIP_CHECK(hipMemcpyAsync(dpk, hp.data() + np, np * sizeof(int32_t),
+    int32_t* hpp = reinterpret_cast<int32_t*>(hsrc_->as<uint64_t>() + 32);
+    std::copy(hp.begin(), hp.end(), hpp);
+    std::copy(hk.begin(), hk.end(), hpp + np1);
+    MSBFS_HIP_CHECK(hipMemcpyAsync(dpv, hpp, (size_t)np1 * 2 * sizeof(int32_t),
                                    hipMemcpyHostToDevice, s));
   }
   ++epoch_;

@@ -161,6 +161,17 @@ def test_cli_gpu_spmd(tmp_path, msbfs_pkg, spmd, comm, dist, K):
     assert js["traversed_edges"] == int(ref.edges.sum())
 
 
+def test_cli_gpu_spmd_rccl_shared_gpu_refused(tmp_path, msbfs_pkg):
+    """--spmd 2 --comm rccl on one GPU (repeated devices, which RCCL rejects) fails
+    with a message instead of running over host collectives unannounced."""
+    m = msbfs_pkg
+    g, qs, gp, qp = _files(tmp_path, m, 100, 4)
+    r = subprocess.run([_cli(m), "-g", gp, "-q", qp, "-gn", "1", "--algo", "bitpar", "--spmd", "2",
+                        "--comm", "rccl"], capture_output=True, text=True, timeout=120,
+                       env={**os.environ, "MSBFS_NO_MPI": "1"})
+    assert r.returncode != 0 and "one GPU per --spmd rank" in (r.stderr + r.stdout)
+
+
 @pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
 def test_cli_gpu_rccl_repeat_multipass(tmp_path, msbfs_pkg):
     """One-rank RCCL over MPI with several solver passes and --repeat 3: the asynchronous
