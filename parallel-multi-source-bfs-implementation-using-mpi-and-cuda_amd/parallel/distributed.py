@@ -95,6 +95,35 @@ def _comm_device(ctx: DistContext):
     return torch.device("cuda", ctx.device) if ctx.backend == "nccl" else torch.device("cpu")
 
 
+_PINNED = {}
+
+
+def _reduce_small(a: np.ndarray, ctx: DistContext, op) -> np.ndarray:
+    """All-reduce of a small host array. Under RCCL the values travel through a cached pinned
+    host buffer and device buffer (per device, dtype and length): pageable host<->device copies
+    stage through the runtime and now and then stalled for milliseconds (the native solver's
+    pageable source copies did, 1 step in 10-30 at +6 ms; tools/step_split.py)."""
+    import torch
+    import torch.distributed as dist
+    dev = _comm_device(ctx)
+    if dev.type != "cuda":
+        t = torch.from_numpy(np.array(a, copy=True))
+        dist.all_reduce(t, op=op)
+        return t.numpy()
+    key = (dev.index, a.dtype.str, a.shape[0])
+    if key not in _PINNED:
+        dt = torch.from_numpy(a[:0]).dtype
+        _PINNED[key] = (torch.empty(a.shape[0], dtype=dt, pin_memory=True),
+                        torch.empty(a.shape[0], dtype=dt, device=dev))
+    h, d = _PINNED[key]
+    h.numpy()[:] = a
+    d.copy_(h, non_blocking=True)
+    dist.all_reduce(d, op=op)
+    h.copy_(d, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    return h.numpy().copy()
+
+
 def barrier(ctx: DistContext) -> None:
     import torch.distributed as dist
     if ctx.distributed:
@@ -189,23 +218,17 @@ def _qbits(K: int) -> int:
 
 
 def allreduce_max(x: float, ctx: DistContext) -> float:
-    import torch
     import torch.distributed as dist
     if not ctx.distributed:
         return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=_comm_device(ctx))
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return float(_reduce_small(np.array([float(x)], np.float64), ctx, dist.ReduceOp.MAX)[0])
 
 
 def allreduce_sum_i64(a: np.ndarray, ctx: DistContext) -> np.ndarray:
-    import torch
     import torch.distributed as dist
     if not ctx.distributed:
         return a
-    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)).to(_comm_device(ctx))
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return t.cpu().numpy()
+    return _reduce_small(np.ascontiguousarray(a, dtype=np.int64), ctx, dist.ReduceOp.SUM)
 
 
 def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistContext,
@@ -216,21 +239,17 @@ def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistC
     62 bits with the query index sends key 0 instead, which every rank then sees as the MIN: all of
     them take the two-all-reduce fallback together.
     """
-    import torch
     import torch.distributed as dist
 
     F_local = np.asarray(F_local, dtype=np.int64)
     idx_local = np.asarray(idx_local, dtype=np.int64)
     qb = _qbits(K)
     NONE = np.iinfo(np.int64).max
-    dev = _comm_device(ctx) if ctx.distributed else None
 
     def allmin(v: int) -> int:
         if not ctx.distributed:
             return v
-        t = torch.tensor([v], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        return int(t.item())
+        return int(_reduce_small(np.array([v], np.int64), ctx, dist.ReduceOp.MIN)[0])
 
     maxF = int(F_local.max()) if len(F_local) else 0
     fits = qb < 62 and (maxF >> (62 - qb)) == 0

@@ -255,11 +255,12 @@ class HybridRunner:
 
         if not self.ctx.distributed:
             return vec
+        if not self._staged:  # (RCCL: through cached pinned buffers, see D._reduce_small)
+            return D._reduce_small(np.ascontiguousarray(vec, dtype=np.int64), self.ctx,
+                                   dist.ReduceOp.SUM)
         t = torch.from_numpy(vec)
-        if not self._staged:
-            t = t.to(self.send.device)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return t.cpu().numpy()
+        return t.numpy()
 
     def run(self, queries, checked: bool = False) -> HybridResult:
         """One hybrid step. checked=True (bench.py's untimed selection pass): every rank-local
