@@ -962,15 +962,13 @@ static __global__ __launch_bounds__(kBlock) void k_chunk_desc(const int32_t* wl,
 // rows), pass 2 only the remaining chunks of the vertices pass 1 left open. In one pass every
 // chunk of a covered vertex still cost its wave an own-row load and a returning atomic before
 // it could skip (RMAT-26 level 3: 313K wide vertices, ~1M+ chunks, 0.5 ms).
-// (plen != nullptr: the prefix-pull level, chunks of the row prefixes with ids < H only)
 static __global__ __launch_bounds__(kBlock) void k_chunk_first(const int32_t* wl, int64_t nw,
                                                                const int64_t* rowptr,
-                                                               const int32_t* plen,
                                                                ChunkDesc* desc, int64_t* cnt) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
        i += (int64_t)gridDim.x * kBlock) {
     const int32_t v = wl[i];
-    const int64_t b = rowptr[v], e = plen ? b + plen[v] : rowptr[v + 1];
+    const int64_t b = rowptr[v], e = rowptr[v + 1];
     desc[i] = ChunkDesc{v, (uint32_t)b, (uint32_t)((uint64_t)b >> 32),
                         (int32_t)min((int64_t)kChunk, e - b)};
   }
@@ -981,8 +979,7 @@ static __global__ __launch_bounds__(kBlock) void k_chunk_first(const int32_t* wl
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_chunk_rest_count(
     const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, const uint64_t* acc,
-    const uint64_t* alive, const uint64_t* gmask, const uint32_t* snap, const int32_t* plen,
-    int64_t* cnt) {
+    const uint64_t* alive, const uint64_t* gmask, const uint32_t* snap, int64_t* cnt) {
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   const int lane = lane_id(), slot = lane % G, sub = lane / G, wv = threadIdx.x >> 6;
@@ -1003,7 +1000,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_rest_count(
     }
     const bool g_open = (__ballot(open) >> (sub * G)) & L::GBITS;
     if (i < nw && slot == 0) {
-      const int64_t d = plen ? (int64_t)plen[v] : rowptr[v + 1] - rowptr[v];
+      const int64_t d = rowptr[v + 1] - rowptr[v];
       const int64_t nc = (d + kChunk - 1) / kChunk;
       cnt[i] = g_open && nc > 1 ? nc - 1 : 0;
     }
@@ -1013,14 +1010,13 @@ __global__ __launch_bounds__(kBlock) void k_chunk_rest_count(
 static __global__ __launch_bounds__(kBlock) void k_chunk_rest_desc(const int32_t* wl, int64_t nw,
                                                                    const int64_t* offs,
                                                                    const int64_t* rowptr,
-                                                                   const int32_t* plen,
                                                                    ChunkDesc* desc) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nw;
        i += (int64_t)gridDim.x * kBlock) {
     const int64_t c0 = i ? offs[i - 1] : 0, c1 = offs[i];
     if (c0 == c1) continue;
     const int32_t v = wl[i];
-    const int64_t b = rowptr[v], e = plen ? b + plen[v] : rowptr[v + 1];
+    const int64_t b = rowptr[v], e = rowptr[v + 1];
     for (int64_t c = c0; c < c1; ++c) {
       const int64_t cb = b + (1 + c - c0) * kChunk;
       desc[c] = ChunkDesc{v, (uint32_t)cb, (uint32_t)((uint64_t)cb >> 32),

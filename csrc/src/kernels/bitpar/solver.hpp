@@ -107,7 +107,6 @@ struct Tuning {
   // two-pass chunk scheduling of the wide vertices on early-exit levels (k_chunk_first):
   // RMAT-26 / 1024 groups level 3 5.70 -> 5.30 ms
   int chunk2 = 1;
-  int chunk2_l2 = 0;  // the same on the prefix-pull level 2 of passes without tiles (early exit)
   // wide threshold of the first pull level for passes of <= 4 words (no tiles there) while
   // SolverOptions::wide_degree is at its default: RMAT-26, level 2, 128 groups 6.54 -> 6.01 ms,
   // 256 groups 7.49 -> 7.11 ms (32 -> 128; 512 and 2048 slower). 0: wide_degree as given

@@ -410,9 +410,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   // bottom-up level (level 2: hardly any row gets covered, and round-robin chunk dealing
   // balances the hubs better). When top-down ran longer (RMAT-30: first pull at level 3, most of
   // every hub's groups already visited) the early exit skips most chunks.
-  // (tuning chunk2_l2: the prefix level too, in two passes, for the passes without tiles)
-  const bool two_l2 = tun_.chunk2_l2 && pfx && !tiled && tun_.chunk2;
-  const int coop = !first_bu || S.level != 2 || two_l2 ? 1 : 0;
+  const int coop = !first_bu || S.level != 2 ? 1 : 0;
   auto launch_chunks = [&](const ChunkDesc* d, const int64_t* np, int64_t maxc) {
     if (hub_lds) {
       // exact chunk count = *np, read on the device (no host round trip); one block per CU
@@ -430,14 +428,14 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     }
     MSBFS_HIP_CHECK(hipGetLastError());
   };
-  if (S.nactw && !tiled && coop && (!pfx || two_l2) && tun_.chunk2) {
+  if (S.nactw && !tiled && coop && !pfx && tun_.chunk2) {
     // two passes (see k_chunk_first): first chunks, then the rest of the open vertices
     const int64_t chunks_max = S.nactw + S.ea / kChunk + 1;
     desc_.ensure((size_t)chunks_max * sizeof(ChunkDesc));
     chunk_cnt_.ensure(sizeof(int64_t));
     ChunkDesc* d = desc_.as<ChunkDesc>();
     k_chunk_first<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
-        actw_[0].as<int32_t>(), S.nactw, g_.rowptr, plen, d, chunk_cnt_.as<int64_t>());
+        actw_[0].as<int32_t>(), S.nactw, g_.rowptr, d, chunk_cnt_.as<int64_t>());
     MSBFS_HIP_CHECK(hipGetLastError());
     launch_chunks(d, chunk_cnt_.as<int64_t>(), S.nactw);
     int64_t* cnt = scan_tmp_.as<int64_t>();
@@ -445,11 +443,11 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     const size_t tb = scan_bytes_ - (size_t)(t2 - (char*)scan_tmp_.p);
     k_chunk_rest_count<W><<<grid_for(S.nactw, L::TILE, grid), kBlock, 0, s>>>(
         actw_[0].as<int32_t>(), S.nactw, g_.rowptr, R, acc_[S.ac].as<uint64_t>(), alive,
-        sm.gmask, snap, plen, cnt);
+        sm.gmask, snap, cnt);
     MSBFS_HIP_CHECK(hipGetLastError());
     inclusive_scan_i64(cnt, offs_.as<int64_t>(), S.nactw, t2, tb, s);
     k_chunk_rest_desc<<<grid_for(S.nactw, kBlock), kBlock, 0, s>>>(
-        actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, plen, d + S.nactw);
+        actw_[0].as<int32_t>(), S.nactw, offs_.as<int64_t>(), g_.rowptr, d + S.nactw);
     MSBFS_HIP_CHECK(hipGetLastError());
     launch_chunks(d + S.nactw, offs_.as<int64_t>() + S.nactw - 1, chunks_max - S.nactw);
   } else if (S.nactw && !tiled) {

@@ -49,7 +49,6 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "dskip3") dskip3 = (int)to_num(key, v);
   else if (key == "hskip") hskip = (int)to_num(key, v);
   else if (key == "chunk2") chunk2 = (int)to_num(key, v);
-  else if (key == "chunk2_l2") chunk2_l2 = (int)to_num(key, v);
   else if (key == "wide_few") wide_few = (int)to_num(key, v);
   else if (key == "tiles_w") {
     tiles_w = (int)to_num(key, v);
@@ -64,7 +63,7 @@ void Tuning::set(const std::string& key, const std::string& v) {
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip first_u push_after dskip3 hskip chunk2 chunk2_l2 wide_few tiles_w dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip first_u push_after dskip3 hskip chunk2 wide_few tiles_w dirs)");
   }
 }
 
