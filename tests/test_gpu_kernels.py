@@ -277,30 +277,6 @@ def test_bitpar_prefix_pull_tail_push(msbfs_pkg):
     g.close()
 
 
-@pytest.mark.parametrize("K", [200, 100, 40])
-def test_bitpar_prefix_level_two_pass_chunks(msbfs_pkg, K):
-    """chunk2_l2: the prefix-pull level 2 of a pass without tiles (4 / 2 / 1 words) runs its hub
-    chunks in two passes with early exit (first chunk of every wide vertex, then the rest of the
-    open ones, chunks over the row prefixes only): same F as one pass, with the wide threshold at
-    its default and at 4 (many wide vertices), and equal to the distance solver on a sample."""
-    m = msbfs_pkg
-    g = m.DeviceGraph.rmat(23, 16, 5, device=0)
-    g.relabel_by_degree()
-    qs = m.QuerySet.random(g.n, K, 16, seed=K + 1)
-    out = {}
-    for wide in (0, 4):
-        for two in (0, 1):
-            with m.Solver(g, "bitpar", max_groups=qs.K, wide_degree=wide,
-                          tuning={"chunk2_l2": two}) as s:
-                out[(wide, two)] = s.run(qs).F
-                out[(wide, two, 2)] = s.run(qs).F
-    for k in out:
-        assert np.array_equal(out[k], out[(0, 0)]), k
-    with m.Solver(g, "dist") as ds:
-        assert np.array_equal(ds.run(qs.subset(np.arange(0, K, 13))).F, out[(0, 1)][::13])
-    g.close()
-
-
 @pytest.mark.parametrize("K", [1024, 900, 512, 200])
 def test_bitpar_tiled_first_pull(msbfs_pkg, K):
     """The first pull level over static vertex tiles (k_pfx_tiles + big-vertex partial tiles +
