@@ -25,7 +25,10 @@ double to_num(const std::string& key, const std::string& v) {
 
 void Tuning::set(const std::string& key, const std::string& v) {
   if (key == "gamma") gamma = to_num(key, v);
-  else if (key == "gamma2") gamma2 = to_num(key, v);
+  else if (key == "gamma2") {
+    gamma2 = to_num(key, v);
+    gamma2_auto = false;
+  }
   else if (key == "pfx") {
     pfx = (int)to_num(key, v);
     if (pfx != 0 && pfx != 2) fail("tuning: pfx must be 0 (whole rows) or 2 (prefix pull)");
