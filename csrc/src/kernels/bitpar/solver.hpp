@@ -109,8 +109,9 @@ struct Tuning {
   // RMAT-26 / 1024 groups level 3 5.70 -> 5.30 ms
   int chunk2 = 1;
   // wide threshold of the first pull level for passes of <= 4 words (no tiles there) while
-  // SolverOptions::wide_degree is at its default: RMAT-26, level 2, 128 groups 6.54 -> 6.01 ms,
-  // 256 groups 7.49 -> 7.11 ms (32 -> 128; 512 and 2048 slower). 0: wide_degree as given
+  // SolverOptions::wide_degree is at its default, on graphs of >= 2^23 non-isolated vertices:
+  // RMAT-26, level 2, 128 groups 6.54 -> 6.01 ms, 256 groups 7.49 -> 7.11 ms (32 -> 128; 512 and
+  // 2048 slower; RMAT-22 prefers 32-64). 0: wide_degree as given
   int wide_few = 128;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a

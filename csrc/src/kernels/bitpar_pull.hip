@@ -183,8 +183,11 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   if (!S.have_active && !tiled) {
     // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
     // off only for much higher degrees, so later lists are split at a higher threshold
+    // (wide_few only on big graphs: RMAT-22 / 64 groups ran level 2 in 0.66 ms at 32 or 64 and
+    // 0.76-0.83 ms at 128; the narrow pull's long rows then have too few vertices to hide behind)
     const int wide0 = S.bu_levels != 0 ? next_wide
-                      : (W <= 4 && tun_.wide_few > 0 && opt.wide_degree == kDefaultWideDegree)
+                      : (W <= 4 && tun_.wide_few > 0 && opt.wide_degree == kDefaultWideDegree &&
+                         n_eff() >= ((int64_t)1 << 23))
                           ? tun_.wide_few
                           : opt.wide_degree;
     k_build_active<4096><<<grid_for(S.cnt, 4096, INT32_MAX), kBlock, 0, s>>>(

@@ -86,18 +86,25 @@ def test_bitpar_two_pass_chunks(msbfs_pkg, wide):
                 assert np.array_equal(s.run(qs).F, ref.F), (name, wide, tun)
 
 
-@pytest.mark.parametrize("wide_few", [0, 8, 128, 1 << 20])
-def test_bitpar_first_pull_wide_threshold(msbfs_pkg, wide_few):
-    """wide_few: the first pull level's wide threshold for passes of <= 4 words (while
-    wide_degree is at its default); 0 keeps wide_degree. Exact F for 1, 2 and 4 words."""
+def test_bitpar_first_pull_wide_threshold(msbfs_pkg):
+    """wide_few: the first pull level's wide threshold for passes of <= 4 words while wide_degree
+    is at its default, on graphs of >= 2^23 non-isolated vertices (a relabelled RMAT-24 here,
+    prefix pull + tail push on level 2); 0 keeps wide_degree. Same F for every threshold at 1, 2
+    and 4 words, equal to the distance solver on a sample."""
     m = msbfs_pkg
-    for name, g in _graphs(m)[:4] + [("rmat14", m.Graph.rmat(14, 16, 5))]:
-        for K in (40, 100, 250):
-            qs = m.QuerySet.random(g.n, K, 6, seed=K)
-            ref = m.cpu_bfs(g, qs)
-            with m.Solver(g.to_device(0), "bitpar", max_groups=K,
-                          tuning={"wide_few": wide_few}) as s:
-                assert np.array_equal(s.run(qs).F, ref.F), (name, K, wide_few)
+    g = m.DeviceGraph.rmat(24, 16, 3, device=0)
+    g.relabel_by_degree()
+    for K in (40, 100, 250):
+        qs = m.QuerySet.random(g.n, K, 16, seed=K)
+        out = {}
+        for wf in (0, 8, 128, 1 << 20):
+            with m.Solver(g, "bitpar", max_groups=K, tuning={"wide_few": wf}) as s:
+                out[wf] = s.run(qs).F
+                assert s.level_trace()[1]["dir"] == "B", (K, wf)  # level 2 pulls
+            assert np.array_equal(out[wf], out[0]), (K, wf)
+        with m.Solver(g, "dist") as ds:
+            assert np.array_equal(ds.run(qs.subset(np.arange(0, K, 17))).F, out[128][::17])
+    g.close()
 
 
 @pytest.mark.parametrize("force_dir,wide", [(1, 64), (2, 64), (2, 2), (0, 8)])
