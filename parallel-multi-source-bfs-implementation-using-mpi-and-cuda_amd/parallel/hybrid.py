@@ -355,7 +355,7 @@ def overlapped_exchange_ms(phase_a_ms: float, ready_ms, piece_bytes, gbps: float
 
 def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
                   coded: Optional[bool] = None, chunks: int = 1,
-                  wbeg: Optional[np.ndarray] = None) -> np.ndarray:
+                  wbeg: Optional[np.ndarray] = None, piece_hook=None) -> np.ndarray:
     """Run the hybrid algorithm for `world` ranks sequentially in ONE process on one GPU (no
     torch.distributed): phase A of every rank, a host-side all-to-all, phase C of every rank.
     Returns the full F vector. Used by the GPU tests and to time per-rank phases: with
@@ -365,7 +365,8 @@ def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
     HybridRunner; each piece's ready time (CUDA events after its pack) and bytes are recorded
     ("pieces") so that tools/hybrid_sim.py can price only the exchange phase A does not hide.
     wbeg: a custom word split (world + 1 non-decreasing entries from 0 to ceil(K/64); default
-    word_split, the even one)."""
+    word_split, the even one). piece_hook(c, nbytes): called after each piece is packed (e.g.
+    to start a one-rank RCCL copy of that size and see what it does to phase A's kernels)."""
     import torch
 
     coded = coding_default() if coded is None else bool(coded)
@@ -394,6 +395,8 @@ def emulate_ranks(solver, queries, world: int, timings: Optional[list] = None,
                 e = torch.cuda.Event(enable_timing=True)
                 e.record()
                 pieces.append((e, 8 * (i1 - i0) * int(wbeg[-1])))
+                if piece_hook is not None:
+                    piece_hook(c, pieces[-1][1])
 
             out, sa = solver.hybrid_phase_a_chunked(queries, r, world, n_eff, r == 0, wbeg,
                                                     buf.data_ptr(), chunks, on_chunk)

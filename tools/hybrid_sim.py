@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--chunks", type=int, default=4,
                     help="overlapped exchange: phase A hands out its vertex ranges in this many "
                          "pieces (1 = the whole exchange after phase A)")
+    ap.add_argument("--rccl-pieces", action="store_true",
+                    help="start a one-rank RCCL all-to-all of each piece's size as it is packed "
+                         "(its kernels then compete with phase A's for the CUs, as on a node)")
     args = ap.parse_args()
 
     import msbfs
@@ -45,6 +48,18 @@ def main():
 
     g = msbfs.DeviceGraph.rmat(args.scale, args.edgefactor, 1, device=0, relabel=True)
     qs = msbfs.QuerySet.random(g.n, args.groups, args.group_size, 7)
+    hook = None
+    if args.rccl_pieces:
+        import torch
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        scratch = [torch.zeros(1 << 27, dtype=torch.int64, device="cuda:0") for _ in range(2)]
+
+        def hook(c, nbytes):
+            n = min(int(nbytes) // 8, scratch[0].numel())
+            dist.all_to_all_single(scratch[1][:n], scratch[0][:n], async_op=True)
     with msbfs.Solver(g, "bitpar", max_groups=qs.K) as s:
         ref = s.run(qs)
         t = time.perf_counter()
@@ -53,9 +68,11 @@ def main():
         print(json.dumps({"ranks": 1, "ms": round(one, 3), "device_ms": ref.stats["device_ms"]}),
               flush=True)
         for N in args.ranks:
-            H.emulate_ranks(s, qs, N, coded=args.coded, chunks=args.chunks)  # warm
+            H.emulate_ranks(s, qs, N, coded=args.coded, chunks=args.chunks,
+                            piece_hook=hook)  # warm
             tim = []
-            F = H.emulate_ranks(s, qs, N, timings=tim, coded=args.coded, chunks=args.chunks)
+            F = H.emulate_ranks(s, qs, N, timings=tim, coded=args.coded, chunks=args.chunks,
+                                piece_hook=hook)
             ok = bool(np.array_equal(F, ref.F))
             a = max(x["phase_a_ms"] for x in tim)
             c = max(x["phase_c_ms"] + x.get("decode_ms", 0.0) for x in tim)  # decode: receiver
