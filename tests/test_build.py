@@ -40,3 +40,38 @@ def test_bench_rejects_world_size_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
                        capture_output=True, text=True, timeout=60, env=env, cwd=ROOT)
     assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_level_record_layout(tmp_path):
+    """The ctypes mirrors of the C API's structs (msbfs_level, msbfs_stats, msbfs_options in
+    msbfs.h) have the C compiler's size and field offsets: the per-level records, run stats and
+    solver options cross the FFI by memory layout."""
+    import ctypes
+
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no host C compiler")
+    from msbfs.ops import native as N
+
+    structs = {"msbfs_level": N.Level, "msbfs_stats": N.Stats, "msbfs_options": N.Options}
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "msbfs/msbfs.h"',
+             "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'  printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    inc = os.path.join(ROOT, "csrc", "include")
+    subprocess.run([cc, "-std=c11", "-I", inc, str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    seen = 0
+    for line in filter(None, out):
+        cname, what, val = line.split()
+        py = structs[cname]
+        got = ctypes.sizeof(py) if what == "size" else getattr(py, what).offset
+        assert got == int(val), (cname, what, got, val)
+        seen += 1
+    assert seen == sum(1 + len(p._fields_) for p in structs.values())
