@@ -127,10 +127,8 @@ __device__ __forceinline__ void wave_set_bits(uint32_t* bm, int32_t v, bool pred
   }
   if ((pending >> lane) & 1ull) atomicOr(&bm[w], bit);
 }
-// flags of the unfiltered pull kernels (k_bu_first, k_bu_full, k_bu_lean)
+// flags of the unfiltered pull kernels (k_bu_first, k_bu_full)
 constexpr int kFlagSkipRows = 1;     // dskip: a vertex finishing here writes no row
-constexpr int kFlagHitSkip = 4;      // k_bu_first: done first neighbour -> finished, row unread
-constexpr int kFlagCountRem = 8;     // k_bu_full: count the groups still unvisited, not new ones
 // anyvis: bit v set once vertex v is visited by any group. A clear bit guarantees both visited
 // buffers of v are all-zero (bits are set before/with the first non-zero store and never
 // cleared within a batch), so pulls may skip the 8*W-byte load; a set bit only costs a load.
@@ -315,20 +313,13 @@ __device__ __forceinline__ bool bu_gate_open(const BuGate& g) {
 // Sum the level's slab rows: block (word, row-group); lane = group bit. F += level * count
 // (`level` is the weight: 0 for a level another rank of the hybrid mode accounts for),
 // alive_next |= groups with count > 0 (one ballot + one atomicOr per word per row-group).
-// cum[i] (when not null) = vertices with edges visited by group i so far (see k_init), kept for
-// the subtractive count: with npos >= 0 (one row group: a block owns its word) the slab rows
-// hold, per group, the vertices still NOT visited after the level (the hit-skip lean level, see
-// k_bu_first), and the level's new count is (npos - cum[i]) - that, for the groups alive
-// (alive_cur) at the level; npos = vertices with edges.
 template <int W, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
                                                          const unsigned long long* slabE, int rows,
                                                          int rgroups, unsigned long long* F,
                                                          unsigned long long* E,
                                                          uint64_t* alive_next, uint32_t level,
-                                                         BuGate gate, unsigned long long* cum,
-                                                         const uint64_t* alive_cur,
-                                                         long long npos) {
+                                                         BuGate gate) {
   if (!bu_gate_open(gate)) return;  // (uniform: no barrier skipped by part of the block)
   __shared__ unsigned long long pf[kWaves][64], pe[kWaves][64];
   const int word = blockIdx.x % W, rg = blockIdx.x / W;
@@ -349,12 +340,6 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce(const uint32_t* slabF,
       f += pf[w][lane];
       e += pe[w][lane];
     }
-    if (npos >= 0) {  // (subtractive level: rgroups == 1)
-      const bool alv = (alive_cur[word] >> lane) & 1ull;
-      const unsigned long long c = cum[i];
-      f = alv ? (unsigned long long)npos - c - f : 0ull;
-    }
-    if (cum && f) atomicAdd(&cum[i], f);  // (several row groups per group i)
     if (f) atomicAdd(&F[i], f * level);
     if constexpr (COUNT) {
       if (e) atomicAdd(&E[i], e);
@@ -374,15 +359,14 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce_multi(const uint32_t* s
                                                                int nlev, int rgroups,
                                                                uint32_t level_first, int weight_l1,
                                                                unsigned long long* F,
-                                                               uint64_t* alive_next,
-                                                               unsigned long long* cum) {
+                                                               uint64_t* alive_next) {
   __shared__ uint32_t pl[kWaves][64];
   const int word = blockIdx.x % W, rg = blockIdx.x / W;
   const int lane = lane_id(), wv = threadIdx.x >> 6;
   const int r0 = (int)((int64_t)rows * rg / rgroups);
   const int r1 = (int)((int64_t)rows * (rg + 1) / rgroups);
   const int i = word * 64 + lane;
-  unsigned long long fw = 0, fc = 0;
+  unsigned long long fw = 0;
   for (int j = 0; j < nlev; ++j) {
     uint32_t f = 0;
     for (int r = r0 + wv; r < r1; r += kWaves) f += slabF[((size_t)j * rows + r) * (64 * W) + i];
@@ -392,14 +376,12 @@ __global__ __launch_bounds__(kBlock) void k_level_reduce_multi(const uint32_t* s
       for (int w = 1; w < kWaves; ++w) f += pl[w][lane];
       const uint32_t lvl = level_first + (uint32_t)j;
       fw += (unsigned long long)f * ((lvl == 1 && !weight_l1) ? 0u : lvl);
-      fc += f;
       const uint64_t m = __ballot(f != 0);
       if (lane == 0 && m) atomicOr((unsigned long long*)&alive_next[16 * j + word], m);
     }
     __syncthreads();
   }
   if (wv == 0 && fw) atomicAdd(&F[i], fw);
-  if (wv == 0 && fc && cum) atomicAdd(&cum[i], fc);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -61,8 +61,7 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_
                                                  uint64_t* visB, uint64_t* acc, int32_t* stamp,
                                                  int32_t epoch, int32_t* fl, Ctr* ctr,
                                                  unsigned long long* E, uint64_t* alive,
-                                                 uint32_t* anyvis, const int32_t* relabel,
-                                                 unsigned long long* cum) {
+                                                 uint32_t* anyvis, const int32_t* relabel) {
   __shared__ LdsQueue q;
   __shared__ unsigned long long scratch[kWaves];
   q_init(q);
@@ -85,7 +84,6 @@ __global__ __launch_bounds__(kBlock) void k_init(const int32_t* pv, const int32_
         (void)alive;  // alive (groups with a valid source) is uploaded by the host
         const unsigned long long deg = (unsigned long long)(rowptr[v + 1] - rowptr[v]);
         if constexpr (COUNT) atomicAdd(&E[k], deg);
-        if (deg > 0) atomicAdd(&cum[k], 1ull);  // (Small::cum counts vertices with edges)
         app = atomicExch(&stamp[v], epoch) != epoch;
         if (app) {
           ef += deg;

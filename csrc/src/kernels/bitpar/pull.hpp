@@ -569,17 +569,13 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
 // dsnap / skip (tuning dskip, see k_bu_full): a first neighbour done at the level start
 // covers every alive group (probe instead of its row); every vertex this pass finishes is done,
 // so with skip it writes no row at all.
-template <int W, bool HS = false>
+template <int W>
 __global__ __launch_bounds__(kBlock, W >= 16 ? 8 : 6) void k_bu_first(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
     int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF, const int32_t* first,
     const uint32_t* dsnap, int flags) {
   const bool skip = flags & kFlagSkipRows;
-  // hit-skip (tuning hskip; needs skip): a vertex whose first neighbour is done in dsnap finishes
-  // with its own row unread (its new bits am & ~row are not needed: the level counts the
-  // vertices left unvisited afterwards, see k_level_reduce), so this pass counts nothing
-  constexpr bool hs = HS;  // (flags & kFlagHitSkip: a separate instantiation, own registers)
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   // done / any-visited bits: one atomic per word of the wave (wave_set_bits) where a wave
@@ -608,33 +604,21 @@ __global__ __launch_bounds__(kBlock, W >= 16 ? 8 : 6) void k_bu_first(
     int32_t v = 0;
     V<VW> r = vzero<VW>(), nw = vzero<VW>();
     uint32_t deg = 0;
-    bool open = false, rnz = false, hitv = false;
+    bool open = false, rnz = false;
     if (valid) {
       v = act[idx];
       const int32_t u = first ? first[v] : col[rowptr[v]];  // active vertices have deg > 0
       V<VW> x;
-      if constexpr (hs) {  // own row only when the probe misses
-        deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);
-        if (dsnap && ((dsnap[u >> 5] >> (u & 31)) & 1u)) {
-          hitv = true;
-        } else {
-          r = ldv<VW>(R + (int64_t)v * W + slot * VW);
-          x = ldv<VW>(R + (int64_t)u * W + slot * VW);
-        }
-      } else {
-        r = ldv<VW>(R + (int64_t)v * W + slot * VW);
-        deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);  // only counted, off the load chain
-        if (dsnap && ((dsnap[u >> 5] >> (u & 31)) & 1u)) x = am;  // (a done first neighbour)
-        else x = ldv<VW>(R + (int64_t)u * W + slot * VW);
-      }
-      if (!hitv) {
+      r = ldv<VW>(R + (int64_t)v * W + slot * VW);
+      deg = (uint32_t)(rowptr[v + 1] - rowptr[v]);  // only counted, off the load chain
+      if (dsnap && ((dsnap[u >> 5] >> (u & 31)) & 1u)) x = am;  // (a done first neighbour)
+      else x = ldv<VW>(R + (int64_t)u * W + slot * VW);
 #pragma unroll
-        for (int j = 0; j < VW; ++j) {
-          const uint64_t unv = ~r.w[j] & am.w[j];
-          nw.w[j] = x.w[j] & unv;
-          open |= (unv & ~nw.w[j]) != 0;
-          rnz |= r.w[j] != 0;
-        }
+      for (int j = 0; j < VW; ++j) {
+        const uint64_t unv = ~r.w[j] & am.w[j];
+        nw.w[j] = x.w[j] & unv;
+        open |= (unv & ~nw.w[j]) != 0;
+        rnz |= r.w[j] != 0;
       }
     }
     const bool g_open = (__ballot(open) >> (sub * G)) & L::GBITS;
@@ -646,28 +630,21 @@ __global__ __launch_bounds__(kBlock, W >= 16 ? 8 : 6) void k_bu_first(
       for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nw.w[j];
       stv<VW>(Wb + (int64_t)v * W + slot * VW, nv);
     }
-    if constexpr (!hs) {
-      bc.add(nw);
-      if (++nadd == (1 << BitCounter<VW>::D) - 1) {
-        bc.template spill_strided32<CR>(cnt, slot);
-        nadd = 0;
-      }
+    bc.add(nw);
+    if (++nadd == (1 << BitCounter<VW>::D) - 1) {
+      bc.template spill_strided32<CR>(cnt, slot);
+      nadd = 0;
     }
     bool anynew = false;
 #pragma unroll
     for (int j = 0; j < VW; ++j) anynew |= nw.w[j] != 0;
-    // (a hit vertex has new bits: it is active, i.e. some alive group has not visited it)
-    const bool g_new = hitv || ((__ballot(anynew) >> (sub * G)) & L::GBITS);
-    const bool g_first = !hitv && g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
+    const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
+    const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
     const bool leader = valid && slot == 0;
     wave_set_bits<kCombine>(done, v, leader && fin);
     if (leader && g_new) ef += deg;
     wave_set_bits<kCombine>(anyvis, v, leader && g_first);
     if (leader && g_first) ev += deg;
-    if (leader && hitv) {  // first visit of a hit vertex: its any-visited bit was still clear
-      const uint32_t m = 1u << (v & 31);
-      if (!(anyvis[v >> 5] & m) && !(atomicOr(&anyvis[v >> 5], m) & m)) ev += deg;
-    }
     q_push(qo, leader && !fin, v);
     q_push(qf, leader && g_new, v);
     q_flush(qo, ovf, &ctr->touched.v, TILE, false);

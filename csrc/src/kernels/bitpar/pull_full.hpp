@@ -8,12 +8,7 @@
 // 3.0 TB/s, ~310 VALU per tile, six block barriers per tile):
 //  * rows move branch-free: a neighbour slot past the end of the row (or a done neighbour) reads
 //    the all-zero row n of the visited buffers (BitparSolver allocates n + 2 rows; levels()
-//    clears rows n and n + 1 for the word count at hand) and an idle lane stores to the scratch
-//    row n + 1. With MSBFS_SBUF (off by default) the rows move with STRUCTURED buffer loads /
-//    stores (index = vertex id, stride = one row, lane offset = its slot: no 64-bit address
-//    arithmetic). Measured on gfx950 (tools/ubench/sbuf_check.hip, round 4): such a descriptor
-//    applies no index range check, and index * stride stops at 4 GiB (every row >= 2^25 of a
-//    128-byte-row buffer read row 2^25 - 1), so MSBFS_SBUF stays off (8.6-GB RMAT-26 buffers);
+//    clears rows n and n + 1 for the word count at hand);
 //  * a step's column ids are broadcast inside the lane group with ds_swizzle (constant pattern,
 //    all CS issued before the first use) instead of one ds_bpermute + wait + branch per row;
 //  * the new lists (next active, next wide, new frontier) go through WAVE-private LDS queues with
@@ -28,89 +23,14 @@
 namespace msbfs {
 namespace bp {
 
-typedef uint32_t bu4 __attribute__((ext_vector_type(4)));
-typedef uint32_t bu2 __attribute__((ext_vector_type(2)));
-// LLVM's structured buffer intrinsics (hipcc exposes only the raw builtins): vindex * stride +
-// voffset from the descriptor base; vindex >= num_records reads zeros and drops stores
-__device__ bu4 sbuf_load_b128(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
-                              int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
-__device__ bu2 sbuf_load_b64(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
-                             int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v2i32");
-__device__ void sbuf_store_b128(bu4 v, __amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset,
-                                int soffset, int aux) __asm("llvm.amdgcn.struct.ptr.buffer.store.v4i32");
-__device__ void sbuf_store_b64(bu2 v, __amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset,
-                               int soffset, int aux) __asm("llvm.amdgcn.struct.ptr.buffer.store.v2i32");
-
-// row slice (VW words) of index u at byte offset voff within the row
-template <int VW>
-__device__ __forceinline__ V<VW> ld_row(__amdgpu_buffer_rsrc_t rs, int32_t u, int voff) {
-  V<VW> r;
-  if constexpr (VW == 2) {
-    const bu4 x = sbuf_load_b128(rs, u, voff, 0, 0);
-    r.w[0] = ((uint64_t)x.y << 32) | x.x;
-    r.w[1] = ((uint64_t)x.w << 32) | x.z;
-  } else {
-    const bu2 x = sbuf_load_b64(rs, u, voff, 0, 0);
-    r.w[0] = ((uint64_t)x.y << 32) | x.x;
-  }
-  return r;
-}
-template <int VW>
-__device__ __forceinline__ void st_row(__amdgpu_buffer_rsrc_t rs, int32_t u, int voff,
-                                       const V<VW>& r) {
-  if constexpr (VW == 2) {
-    bu4 x;
-    x.x = (uint32_t)r.w[0];
-    x.y = (uint32_t)(r.w[0] >> 32);
-    x.z = (uint32_t)r.w[1];
-    x.w = (uint32_t)(r.w[1] >> 32);
-    sbuf_store_b128(x, rs, u, voff, 0, 0);
-  } else {
-    bu2 x;
-    x.x = (uint32_t)r.w[0];
-    x.y = (uint32_t)(r.w[0] >> 32);
-    sbuf_store_b64(x, rs, u, voff, 0, 0);
-  }
-}
-
-#ifndef MSBFS_SBUF
-#define MSBFS_SBUF 0
-#endif
-// The rows of one visited buffer: row u's slice of a lane at byte offset voff (u < n + 2)
-template <int W>
-struct RowBuf {
-#if MSBFS_SBUF
-  __amdgpu_buffer_rsrc_t rs;
-#else
-  uint64_t* base;
-#endif
-};
-template <int W>
-__device__ __forceinline__ RowBuf<W> row_buf(const uint64_t* base, int64_t n) {
-#if MSBFS_SBUF
-  static_assert(W * 8 < 16384, "descriptor stride");
-  return RowBuf<W>{__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)(W * 8), (int)(n + 2),
-                                                     0x00020000)};
-#else
-  (void)n;
-  return RowBuf<W>{(uint64_t*)base};
-#endif
+// row u's slice of a lane at byte offset voff within the row (u < n + 2)
+template <int W, int VW>
+__device__ __forceinline__ V<VW> ld_row(const uint64_t* base, int32_t u, int voff) {
+  return ldv<VW>(base + (int64_t)u * W + voff / 8);
 }
 template <int W, int VW>
-__device__ __forceinline__ V<VW> ld_row(const RowBuf<W>& b, int32_t u, int voff) {
-#if MSBFS_SBUF
-  return ld_row<VW>(b.rs, u, voff);
-#else
-  return ldv<VW>(b.base + (int64_t)u * W + voff / 8);
-#endif
-}
-template <int W, int VW>
-__device__ __forceinline__ void st_row(const RowBuf<W>& b, int32_t u, int voff, const V<VW>& r) {
-#if MSBFS_SBUF
-  st_row<VW>(b.rs, u, voff, r);
-#else
-  stv<VW>(b.base + (int64_t)u * W + voff / 8, r);
-#endif
+__device__ __forceinline__ void st_row(uint64_t* base, int32_t u, int voff, const V<VW>& r) {
+  stv<VW>(base + (int64_t)u * W + voff / 8, r);
 }
 
 // lanes below this one among the set bits of a wave mask (v_mbcnt)
@@ -233,9 +153,10 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   int32_t* qf = qa + QA;
   int32_t* qw = qf + QF;
   uint32_t na = 0, nf = 0, nw = 0;  // (wave-uniform)
-  const RowBuf<W> rR = row_buf<W>(R, n), rO = row_buf<W>(Wb, n);
+  const uint64_t* rR = R;
+  uint64_t* rO = Wb;
   const int voff = slot * VW * 8;
-  const int32_t zrow = (int32_t)n;  // the all-zero row
+  const int32_t zrow = (int32_t)n;  // the all-zero row (n <= INT32_MAX - 2, see the solver)
   V<VW> am;
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
@@ -431,14 +352,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
       for (int j = 0; j < VW; ++j) nv.w[j] = r.w[j] | nwv.w[j];
       if (valid && (g_nf || !skip)) st_row<W, VW>(rO, v, voff, nv);
     }
-    if (flags & kFlagCountRem) {  // (uniform; the overflow of a hit-skip lean pass)
-      V<VW> rem;
-#pragma unroll
-      for (int j = 0; j < VW; ++j) rem.w[j] = unv.w[j] & ~nwv.w[j];
-      bc.add(rem);
-    } else {
-      bc.add(nwv);  // (zero for invalid lanes)
-    }
+    bc.add(nwv);  // (zero for invalid lanes)
     if (++nadd == (1 << decltype(bc)::D) - 1) {
       bc.template spill_strided32<CR>(cnt, slot);
       nadd = 0;
@@ -468,130 +382,6 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   wq_flush_block(qw, nw, actw2, &ctr->actw2.v, wbase);
   wq_flush_block(qf, nf, fl2, &ctr->fl2.v, wbase);
   block_sum_add(eu, &ctr->eu2.v, scratch);
-  block_sum_add(ef, &ctr->ef2.v, scratch);
-  block_sum_add(ev, &ctr->ev2.v, scratch);
-  bc.template spill_strided32<CR>(cnt, slot);
-  __syncthreads();
-  uint32_t* row = slabF + (size_t)blockIdx.x * (64 * W);
-  for (int i = threadIdx.x; i < 64 * W; i += kBlock) row[i] = cnt[i + (i >> 6)];
-}
-
-// The lean first-row pass (k_bu_first's job, tuning key first_u = U > 0) with U tiles per wave
-// and iteration. k_bu_first's loop is one chain of four dependent loads per tile (list entry ->
-// first neighbour id -> done probe -> neighbour row; RMAT-26 level 4: 24.8M vertices, 1.6 ms, the
-// address unit 45 % busy) and four block barriers per tile (two block queues). Here every stage
-// is issued for U tiles before the next stage waits, rows move branch-free (the all-zero row n
-// for a probed or idle slot, loads skipped when no lane of the wave needs them), the new lists
-// go through wave queues (no barrier in the loop), and a finished vertex's row store is skipped
-// as a whole instruction when no lane of the wave stores (dskip: every finished row).
-template <int W, int U>
-constexpr int lean_occ() { return U <= 1 ? (W >= 16 ? 8 : 6) : (U == 2 ? 5 : 4); }
-template <int W, int U>
-__global__ __launch_bounds__(kBlock, (lean_occ<W, U>())) void k_bu_lean(
-    const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
-    const uint64_t* R, uint64_t* Wb, int64_t n, const uint64_t* alive, const uint64_t* gmask,
-    uint32_t* done, int32_t* ovf, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, uint32_t* slabF,
-    const int32_t* first, const uint32_t* dsnap, int flags) {
-  const bool skip = flags & kFlagSkipRows;
-  using L = Lay<W>;
-  constexpr int VW = L::VW, G = L::G, VPW = L::VPW;
-  constexpr int WT = U * VPW;  // list entries per wave and iteration
-  constexpr bool kCombine = G <= 4;
-  constexpr int CR = 65;
-  constexpr int QF = 1024, QO = 2 * WT > 256 ? 2 * WT : 256;
-  __shared__ int32_t qmem[kWaves][QF + QO];
-  __shared__ unsigned long long scratch[kWaves];
-  __shared__ uint32_t wbase[kWaves + 1];
-  __shared__ uint32_t cnt[CR * W];
-  for (int i = threadIdx.x; i < CR * W; i += kBlock) cnt[i] = 0;
-  __syncthreads();
-  const int lane = lane_id(), slot = lane % G, sub = lane / G;
-  const int wv = threadIdx.x >> 6;
-  int32_t* qf = qmem[wv];
-  int32_t* qo = qf + QF;
-  uint32_t nqf = 0, nqo = 0;  // (wave-uniform)
-  const RowBuf<W> rR = row_buf<W>(R, n), rO = row_buf<W>(Wb, n);
-  const int voff = slot * VW * 8;
-  const int32_t zrow = (int32_t)n, srow = (int32_t)n + 1;
-  V<VW> am;
-#pragma unroll
-  for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
-  unsigned long long ef = 0, ev = 0;
-  BitCounter<VW> bc;
-  bc.zero();
-  int nadd = 0;
-  const int64_t step = (int64_t)gridDim.x * kWaves * WT;
-  for (int64_t tb = ((int64_t)blockIdx.x * kWaves + wv) * WT; tb < nact; tb += step) {
-    int32_t v[U], u[U];
-    bool valid[U], hit[U];
-    uint32_t deg[U];
-    V<VW> r[U], x[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {  // stage 1: list entries (clamped: no branch around a load)
-      const int64_t idx = tb + k * VPW + sub;
-      valid[k] = idx < nact;
-      v[k] = act[valid[k] ? idx : nact - 1];
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) {  // stage 2: first neighbour, own row, offsets
-      const int64_t b = rowptr[v[k]], e = rowptr[v[k] + 1];
-      deg[k] = (uint32_t)(e - b);  // (active vertices have deg > 0)
-      u[k] = first ? first[v[k]] : col[b];
-      r[k] = ld_row<W, VW>(rR, v[k], voff);
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) hit[k] = dsnap && done_in(dsnap, u[k]);  // stage 3: probes
-#pragma unroll
-    for (int k = 0; k < U; ++k) {  // stage 4: rows of the first neighbours not done
-      const bool need = valid[k] && !hit[k];
-      x[k] = vzero<VW>();
-      if (__ballot(need)) x[k] = ld_row<W, VW>(rR, need ? u[k] : zrow, voff);
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      V<VW> nw;
-      bool open = false, rnz = false;
-#pragma unroll
-      for (int j = 0; j < VW; ++j) {
-        const uint64_t xj = hit[k] ? am.w[j] : x[k].w[j];
-        const uint64_t unv = ~r[k].w[j] & am.w[j];
-        nw.w[j] = xj & unv;
-        open |= (unv & ~nw.w[j]) != 0;
-        rnz |= r[k].w[j] != 0;
-      }
-      const bool g_open = (__ballot(open) >> (sub * G)) & L::GBITS;
-      const bool fin = valid[k] && !g_open;
-      if (!fin) nw = vzero<VW>();
-      const bool st = fin && !skip;
-      if (__ballot(st)) {
-        V<VW> nv;
-#pragma unroll
-        for (int j = 0; j < VW; ++j) nv.w[j] = r[k].w[j] | nw.w[j];
-        st_row<W, VW>(rO, st ? v[k] : srow, voff, nv);
-      }
-      bc.add(nw);
-      if (++nadd == (1 << decltype(bc)::D) - 1) {
-        bc.template spill_strided32<CR>(cnt, slot);
-        nadd = 0;
-      }
-      bool anynew = false;
-#pragma unroll
-      for (int j = 0; j < VW; ++j) anynew |= nw.w[j] != 0;
-      const bool g_new = (__ballot(anynew) >> (sub * G)) & L::GBITS;
-      const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
-      const bool leader = valid[k] && slot == 0;
-      wave_set_bits<kCombine>(done, v[k], leader && fin);
-      if (leader && g_new) ef += deg[k];
-      wave_set_bits<kCombine>(anyvis, v[k], leader && g_first);
-      if (leader && g_first) ev += deg[k];
-      wq_push(qo, nqo, leader && !fin, v[k]);
-      wq_push(qf, nqf, leader && g_new, v[k]);
-    }
-    if (nqo + WT > QO) wq_flush(qo, nqo, ovf, &ctr->touched.v);
-    if (nqf + WT > QF) wq_flush(qf, nqf, fl2, &ctr->fl2.v);
-  }
-  wq_flush_block(qo, nqo, ovf, &ctr->touched.v, wbase);
-  wq_flush_block(qf, nqf, fl2, &ctr->fl2.v, wbase);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
   bc.template spill_strided32<CR>(cnt, slot);

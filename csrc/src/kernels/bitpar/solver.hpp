@@ -70,7 +70,6 @@ struct Tuning {
   // least lean_min vertices (RMAT-26 level 4: 2.48 -> 2.07 ms)
   int lean = 1;
   int64_t lean_min = 1 << 20;
-  int lean_level = 3;  // first pull level (1-based) that may run lean
   int lazy = 1;        // no per-batch fill of the visited buffer (see start_batch)
   int td_fused = 1;    // device-driven batches run the one-kernel k_td_fused levels
   int64_t td_bm = 65536;  // k_td_fused walks the frontier bitmap from this frontier size on
@@ -88,9 +87,6 @@ struct Tuning {
   // instead of gathering done neighbours' rows, and the rows of vertices finishing on an
   // unfiltered pull level are not written (a push level right after gets them restored)
   int dskip = 1;
-  // lean pass kernel: 0 = k_bu_first (one tile per wave and iteration), 2 / 4 = k_bu_lean with
-  // that many tiles per wave in flight (bitpar/pull_full.hpp)
-  int first_u = 0;
   // tiled first pull level: the tail push after the tiles, into the output rows (one GPU, no
   // chunked exchange; k_push_tail_after) instead of into acc rows every tile vertex reads
   // (RMAT-26 / 1024 groups: level 2 12.5 -> 10.95 ms, 20.7-21.3 -> 19.1-19.8 ms per step)
@@ -98,13 +94,6 @@ struct Tuning {
   // dskip on the non-lean unfiltered full pulls too (RMAT-26 level 3: 5.80 -> 5.68 ms, 1 GB of
   // row stores fewer; see level_bu)
   int dskip3 = 1;
-  // hit-skip lean pass: a vertex whose first neighbour was done at the level start finishes
-  // without its own row being read; the level counts the vertices still unvisited per group
-  // afterwards instead of the new ones (k_bu_first, k_level_reduce). Exact, but measured slower
-  // (RMAT-26 / 1024 groups: level 4 1.72 -> 1.94 ms; 128 groups 0.67 -> 0.77 ms): few first
-  // neighbours are done at level 4 (late groups keep even the top hubs open), so most vertices
-  // take the longer chain (own row only after the probe)
-  int hskip = 0;
   // two-pass chunk scheduling of the wide vertices on early-exit levels (k_chunk_first):
   // RMAT-26 / 1024 groups level 3 5.70 -> 5.30 ms
   int chunk2 = 1;
@@ -184,9 +173,7 @@ class BitparSolver final : public Solver {
     // dskip: the last level skipped the rows of the vertices it finished; a push level next
     // restores those of its frontier (k_fix_done_rows) from the read buffer and this alive mask
     bool keep_rows = false;
-    bool push_after = false;
-    bool cum_ok = false;      // Small::cum counts every level of this run (not hybrid phase C)
-    bool sub_reduce = false;  // this level's slab rows hold not-visited counts (hit-skip lean pass)  // this tiled level's tail push runs after the tiles (k_push_tail_after)             // every row written (hybrid phase A packs them)
+    bool push_after = false;  // this tiled level's tail push runs after the tiles (k_push_tail_after)
     bool skip_pending = false;
     const uint64_t* skip_alive = nullptr;
     // a level skipped rows: every later pull level of the batch probes dsnap_ (re-snapshotted
@@ -198,7 +185,6 @@ class BitparSolver final : public Solver {
     unsigned long long* E;
     uint64_t* alive[2];
     uint64_t* gmask;
-    unsigned long long* cum;  // per group: vertices with edges visited so far (k_level_reduce)
   };
 
  private:
@@ -209,7 +195,6 @@ class BitparSolver final : public Solver {
     r.alive[0] = (uint64_t*)(r.E + 64 * 16);
     r.alive[1] = r.alive[0] + 16;
     r.gmask = r.alive[1] + 16;
-    r.cum = (unsigned long long*)(r.gmask + 32);
     return r;
   }
   template <int W>
@@ -255,6 +240,12 @@ class BitparSolver final : public Solver {
   // the tiles of the own vertices (part of nparts; built on first use and cached per graph
   // buffers; nullptr for fewer than 8 words, or when they do not fit in HBM)
   const TileSet* pfx_tiles(int W, int part, int nparts, hipStream_t s);
+  // some word count of this solver may take the tiled first pull level (the graph-side half of
+  // level_bu's `tiled` test; pfx_tiles adds the word-count half: W >= 4 and W >= tiles_w)
+  bool tiles_possible() const {
+    return tun_.tiles && tun_.pfx == 2 && g_.rows_sorted && g_.n <= INT32_MAX && maxW_ >= 4 &&
+           maxW_ >= tun_.tiles_w;
+  }
   template <int W>
   int tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t* O, const uint32_t* snap,
                  const uint32_t* codes, int32_t code_from, int rows);
@@ -321,9 +312,6 @@ class BitparSolver final : public Solver {
     return n_eff_;
   }
 
-  // vertices with deg > 0 (cached per graph buffers; the subtractive count of the hit-skip
-  // lean pass, bitpar_pull.hip)
-  int64_t npos(hipStream_t s);
 
   HostCtr read_ctr(hipStream_t s) {
     MSBFS_HIP_CHECK(hipMemcpyAsync(hctr_->p, ctr_.p, sizeof(Ctr), hipMemcpyDeviceToHost, s));
@@ -352,6 +340,10 @@ class BitparSolver final : public Solver {
   // after a few levels (uniform n = 16M, m = 128M, 1024 groups: 29.6 ms vs 32.3 ms fused)
   static constexpr double kTdFusedDeg = 8.0;
   static constexpr int kBatch = 64;  // most levels per device-driven batch
+  static constexpr int kLeanLevel = 3;  // first pull level (1-based) that may run the lean pass
+  // k_bu_full: the all-zero row n is an int32 vertex index (row n + 1 is scratch), so graphs
+  // with n > INT32_MAX - 2 keep k_bu_narrow
+  bool full_pull() const { return tun_.full && g_.n <= (int64_t)INT32_MAX - 2; }
 
   const DeviceGraph& g_;
   Tuning tun_;
@@ -363,8 +355,6 @@ class BitparSolver final : public Solver {
   int32_t epoch_ = 0;
   int64_t n_eff_ = 0;
   const void* eff_key_[3] = {nullptr, nullptr, nullptr};
-  int64_t npos_ = -1;
-  const void* npos_key_[2] = {nullptr, nullptr};
   DevBuf plen_;
   DevBuf chunk_cnt_;  // pass-1 chunk count of the two-pass wide pull (device int64)
   DevBuf first_;

@@ -34,13 +34,6 @@
 #include "common.hpp"
 #include "pull.hpp"
 
-#ifndef TILE_SLICES
-#define TILE_SLICES 5
-#endif
-#ifndef TILE_NH
-#define TILE_NH 1
-#endif
-
 namespace msbfs {
 namespace bp {
 
@@ -196,7 +189,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
   }
   // 5 slices: a spill (one LDS add per set counter bit, ~100 per lane at level 2) every 31
   // passes (6 slices do not fit the 128 VGPRs of a 1024-thread block at 16 words)
-  BitCounter<VW, TILE_SLICES> bc;
+  BitCounter<VW, 5> bc;
   bc.zero();
   int nadd = 0;
   const int64_t nwaves = (int64_t)gridDim.x * NWV;
@@ -332,7 +325,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
         const uint64_t bput = ACC ? bok : __ballot(lane < nv && degl > 0);
         uint32_t m_done = 0, m_new = 0, m_first = 0;
         // two passes per batch: own rows and pushed rows of 16 vertices in flight
-        constexpr int NH = TILE_NH;
+        constexpr int NH = 1;
 #pragma unroll
         for (int h = 0; h < NP; h += NH) {
           if (h * VPW >= nv) break;

@@ -71,24 +71,6 @@ int32_t BitparSolver::code_bound(double min_deg) {
   return deg_bounds_[k];
 }
 
-int64_t BitparSolver::npos(hipStream_t s) {
-  if (npos_key_[0] != (const void*)g_.rowptr || npos_key_[1] != (const void*)g_.col) {
-    DevBuf c;
-    c.alloc(sizeof(unsigned long long));
-    MSBFS_HIP_CHECK(hipMemsetAsync(c.p, 0, sizeof(unsigned long long), s));
-    k_count_wide<<<grid_for(g_.n, kBlock, 2048), kBlock, 0, s>>>(g_.rowptr, g_.n, 0,
-                                                                 c.as<unsigned long long>());
-    MSBFS_HIP_CHECK(hipGetLastError());
-    unsigned long long h = 0;
-    MSBFS_HIP_CHECK(hipMemcpyAsync(&h, c.p, sizeof(h), hipMemcpyDeviceToHost, s));
-    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
-    npos_ = (int64_t)h;
-    npos_key_[0] = g_.rowptr;
-    npos_key_[1] = g_.col;
-  }
-  return npos_;
-}
-
 // Everything a run would otherwise build or allocate on first use, so that no timed run pays
 // for it (the CLI's computation phase, main.cu:301-400): the vertex extent, the prefix
 // lengths and first-neighbour array, the degree-bound table, and the worst-case chunk
@@ -98,10 +80,9 @@ void BitparSolver::prepare(hipStream_t s) {
   constexpr int32_t kPfxH = 14336 * 32;  // (the prefix pull's bound, see level_bu)
   if (g_.rows_sorted && g_.n <= INT32_MAX && tun_.pfx == 2) {
     prefix_lens(kPfxH, s);
-    if (maxW_ >= 8) (void)pfx_tiles(maxW_, 0, 1, s);  // (the first pull level's tiles)
+    if (tiles_possible()) (void)pfx_tiles(maxW_, 0, 1, s);  // (the first pull level's tiles)
   }
   if (tun_.lean) first_nbr(s);
-  (void)npos(s);
   (void)code_bound(1.0);
   DevBuf c;
   c.alloc(sizeof(unsigned long long));
@@ -244,18 +225,18 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   // level never follows it in a batch (ev only grows), and the unfiltered kernels all probe
   // (k_bu_full, k_bu_first, the hub chunks; not the per-vertex pulls of tun_.full = 0)
   const bool lean_now = tun_.lean && !S.lean_off && FUSE && filter_from == INT32_MAX &&
-                        !tiled && !pfx && S.bu_levels >= tun_.lean_level &&
+                        !tiled && !pfx && S.bu_levels >= kLeanLevel &&
                         S.nact >= tun_.lean_min;
-  const bool skip_now = lean_now && !COUNT && tun_.dskip && tun_.full && !S.keep_rows;
+  const bool skip_now = lean_now && !COUNT && tun_.dskip && full_pull() && !S.keep_rows;
   // dskip3: the full pull of an unfiltered, non-lean level (RMAT-26 level 3) skips the rows of
   // the vertices it finishes too, but probes nothing itself while no earlier level skipped (its
   // input rows are all current); the later levels probe as after any skipping level
-  const bool skip3 = !lean_now && tun_.dskip3 && tun_.dskip && !COUNT && tun_.full &&
+  const bool skip3 = !lean_now && tun_.dskip3 && tun_.dskip && !COUNT && full_pull() &&
                      !S.keep_rows && filter_from == INT32_MAX && !tiled && !pfx &&
                      S.bu_levels >= 1;
   const bool probed_before = S.skipped_any;
   const uint32_t* dsnap =
-      (!COUNT && tun_.full) ? done_probe(S, skip_now || skip3, s) : nullptr;
+      (!COUNT && full_pull()) ? done_probe(S, skip_now || skip3, s) : nullptr;
   const uint32_t* dprobe = skip3 && !probed_before ? nullptr : dsnap;
   S.skip_pending = skip_now || skip3;
   S.skip_alive = alive;
@@ -338,42 +319,25 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       // then most vertices are covered by their first neighbour (RMAT-26, 1024 groups: level
       // 4 3.1 -> 2.5 ms; level 3 prefers full steps: 6.5 vs 6.7 ms)
       const bool short1 = S.bu_levels >= 3 || W <= 4;
-      if (tun_.lean && !S.lean_off && FUSE && !filt && S.bu_levels >= tun_.lean_level &&
+      if (tun_.lean && !S.lean_off && FUSE && !filt && S.bu_levels >= kLeanLevel &&
           S.nact >= tun_.lean_min) {
         S.lean_ran = true;
-        // lean first pass, then the regular pull over the vertices it could not finish.
-        // hit-skip (tuning hskip): see k_bu_first; the level's counts become subtractive
-        // (every active vertex is on the narrow list and every level so far fed Small::cum)
-        const bool hs = tun_.hskip && skip_now && dsnap && tun_.full && !tun_.first_u &&
-                        S.nactw == 0 && S.cum_ok;
-        S.sub_reduce = hs;
-        int gl;
-        if (tun_.first_u) {
-          gl = grid_for(S.nact, L::TILE * tun_.first_u, grid);
-          auto kl = tun_.first_u == 4 ? k_bu_lean<W, 4> : k_bu_lean<W, 2>;
-          kl<<<gl, kBlock, 0, s>>>(
-              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
-              done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
-              (skip_now ? kFlagSkipRows : 0));
-        } else {
-          gl = grid_for(S.nact, L::TILE, grid);
-          auto kb = hs ? k_bu_first<W, true> : k_bu_first<W, false>;
-          kb<<<gl, kBlock, 0, s>>>(
-              act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
-              done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
-              ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
-              (skip_now ? kFlagSkipRows : 0) | (hs ? kFlagHitSkip : 0));
-        }
+        // lean first pass, then the regular pull over the vertices it could not finish
+        const int gl = grid_for(S.nact, L::TILE, grid);
+        k_bu_first<W><<<gl, kBlock, 0, s>>>(
+            act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
+            done_.as<uint32_t>(), touched_.as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
+            ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), slabF<W>(rows), first_nbr(s), dsnap,
+            skip_now ? kFlagSkipRows : 0);
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gl;
-        if (tun_.full)
+        if (full_pull())
           k_bu_full<W, full_cs<W>(), 1><<<gn, kBlock, 0, s>>>(
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive, sm.gmask,
               done_.as<uint32_t>(), act_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
               ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), actw_[1].as<int32_t>(), next_wide,
               slabF<W>(rows), &ctr_.as<Ctr>()->touched.v, BuGate{}, dsnap,
-              (skip_now ? kFlagSkipRows : 0) | (hs ? kFlagCountRem : 0));
+              skip_now ? kFlagSkipRows : 0);
         else
           k_bu_narrow<W, COUNT, kBlock, 0, FUSE, false, false, 8, 1><<<gn, kBlock, 0, s>>>(
               touched_.as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive, sm.gmask,
@@ -383,7 +347,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
               &ctr_.as<Ctr>()->touched.v, nullptr, BuGate{});
         MSBFS_HIP_CHECK(hipGetLastError());
         rows += gn;
-      } else if (FUSE && !filt && tun_.full) {
+      } else if (FUSE && !filt && full_pull()) {
         auto kf = short1 ? k_bu_full<W, full_cs<W>(), 1> : k_bu_full<W, full_cs<W>(), 0>;
         kf<<<gn, kBlock, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, n, alive,
                                  sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
@@ -548,7 +512,7 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
   const auto t0 = std::chrono::steady_clock::now();
   trace::Range range_batch("bitpar L%u-%u BU batch", level0 + 1, level0 + K);
   auto kn = k_bu_narrow<W, false, kBlock, 0, true, false, false, 8, 1>;
-  const bool full = tun_.full != 0;
+  const bool full = full_pull();
   // dskip: after a skipping level the batch's levels probe the snapshot (taken once, before the
   // first of them); they skip nothing themselves
   const uint32_t* dsnap = full ? done_probe(S, false, s) : nullptr;
@@ -580,7 +544,7 @@ void BitparSolver::bu_batch(Loop& S, RunStats* st, hipStream_t s) {
              &slots[i].actw2.v, gate, p);
     k_level_reduce<W, false><<<W * rg, kBlock, 0, s>>>(slabF<W>(0), slabE<W>(0), rows, rg, sm.F,
                                                        sm.E, aslot + 16 * (i + 1), level0 + 1 + i,
-                                                       gate, sm.cum, nullptr, -1ll);
+                                                       gate);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   MSBFS_HIP_CHECK(hipMemcpyAsync(hbctr_->p, bctr_.p, (size_t)(K + 1) * sizeof(Ctr),

@@ -133,7 +133,7 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
     if (pend < 0) return;
     k_level_reduce_multi<W><<<W * rg, kBlock, 0, s>>>(slabF_.as<uint32_t>(), grid, upto - pend,
                                                       rg, level0 + 1 + pend, S.weight_l1 ? 1 : 0,
-                                                      sm.F, aslot + 16 * (pend + 1), sm.cum);
+                                                      sm.F, aslot + 16 * (pend + 1));
     MSBFS_HIP_CHECK(hipGetLastError());
     aidx = upto;
     pend = -1;
@@ -190,8 +190,7 @@ void BitparSolver::td_batch(Loop& S, RunStats* st, hipStream_t s) {
           slabF_.as<uint32_t>(), slabE_.as<unsigned long long>());
     k_level_reduce<W, COUNT><<<W * rg, kBlock, 0, s>>>(slabF_.as<uint32_t>(),
                                                        slabE_.as<unsigned long long>(), grid, rg,
-                                                       sm.F, sm.E, aslot + 16 * (i + 1), weight, BuGate{},
-                                                       sm.cum, nullptr, -1ll);
+                                                       sm.F, sm.E, aslot + 16 * (i + 1), weight, BuGate{});
     MSBFS_HIP_CHECK(hipGetLastError());
     aidx = i + 1;
     S.fc ^= 1;

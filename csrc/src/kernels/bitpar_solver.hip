@@ -36,7 +36,6 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "code_deg") code_deg = to_num(key, v);
   else if (key == "lean") lean = (int)to_num(key, v);
   else if (key == "lean_min") lean_min = (int64_t)to_num(key, v);
-  else if (key == "lean_level") lean_level = (int)to_num(key, v);
   else if (key == "lazy") lazy = (int)to_num(key, v);
   else if (key == "td_fused") td_fused = (int)to_num(key, v);
   else if (key == "td_bm") td_bm = (int64_t)to_num(key, v);
@@ -50,23 +49,19 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "dskip") dskip = (int)to_num(key, v);
   else if (key == "push_after") push_after = (int)to_num(key, v);
   else if (key == "dskip3") dskip3 = (int)to_num(key, v);
-  else if (key == "hskip") hskip = (int)to_num(key, v);
   else if (key == "chunk2") chunk2 = (int)to_num(key, v);
   else if (key == "wide_few") wide_few = (int)to_num(key, v);
   else if (key == "tiles_w") {
     tiles_w = (int)to_num(key, v);
     if (tiles_w != 4 && tiles_w != 8 && tiles_w != 16) fail("tuning: tiles_w must be 4, 8 or 16");
   }
-  else if (key == "first_u") {
-    first_u = (int)to_num(key, v);
-    if (first_u != 0 && first_u != 2 && first_u != 4) fail("tuning: first_u must be 0, 2 or 4");
-  } else if (key == "dirs") {
+  else if (key == "dirs") {
     for (char c : v)
       if (c != 'T' && c != 'B' && c != '.') fail("tuning: dirs takes T, B or . per level");
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lean_level lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip first_u push_after dskip3 hskip chunk2 wide_few tiles_w dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip push_after dskip3 chunk2 wide_few tiles_w dirs)");
   }
 }
 
@@ -136,7 +131,7 @@ BitparSolver::BitparSolver(const DeviceGraph& g, int max_groups)
   scan_bytes_ = frontier_scan_temp_bytes(n);
   scan_tmp_.alloc(scan_bytes_);
   ctr_.alloc(sizeof(Ctr));
-  // F, E, alive x 2, gmask, (spare), cum (see Small)
+  // F, E, alive x 2, gmask, (spare) (see Small)
   small_.alloc(64 * 16 * sizeof(unsigned long long) * 3 + 4 * 16 * sizeof(uint64_t));
   // per-level counter slab: <= 3 counting kernels per level x <= kMaxGrid blocks
   slabF_.alloc((size_t)3 * kMaxGrid * 64 * maxW_ * sizeof(uint32_t));
@@ -243,7 +238,7 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
     k_init<W, COUNT><<<grid_for(np, kBlock), kBlock, 0, s>>>(
         dpv, dpk, np, g_.rowptr, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
         acc_[S.ac].as<uint64_t>(), stamp_.as<int32_t>(), epoch_, fl_[S.fc].as<int32_t>(),
-        ctr_.as<Ctr>(), sm.E, sm.alive[0], anyvis_.as<uint32_t>(), g_.old2new, sm.cum);
+        ctr_.as<Ctr>(), sm.E, sm.alive[0], anyvis_.as<uint32_t>(), g_.old2new);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   const HostCtr c = read_ctr(s);  // also retires the pinned/host source copies
@@ -317,15 +312,12 @@ void BitparSolver::levels(Loop& S, RunStats* st, hipStream_t s) {
     const int rows = bottom_up ? level_bu<W, COUNT>(S, s) : level_td<W, COUNT>(S, s);
     if (st) ++(bottom_up ? st->bu_levels : st->td_levels);
     if (rows) {
-      // (a subtractive level: one row group, every block owns its groups' cum entries)
-      const int rg = S.sub_reduce ? 1 : std::max(1, std::min(64, rows / 32));
+      const int rg = std::max(1, std::min(64, rows / 32));
       const uint32_t weight = (S.level == 1 && !S.weight_l1) ? 0u : S.level;
       k_level_reduce<W, COUNT><<<W * rg, kBlock, 0, s>>>(
-          slabF<W>(0), slabE<W>(0), rows, rg, sm.F, sm.E, sm.alive[S.alv ^ 1], weight, BuGate{},
-          sm.cum, sm.alive[S.alv], S.sub_reduce ? (long long)npos(s) : -1ll);
+          slabF<W>(0), slabE<W>(0), rows, rg, sm.F, sm.E, sm.alive[S.alv ^ 1], weight, BuGate{});
       MSBFS_HIP_CHECK(hipGetLastError());
     }
-    S.sub_reduce = false;
     c = read_ctr(s);
     if (S.lean_ran) {
       // (high-diameter graphs: most vertices need more than their first neighbour; once a lean
@@ -377,7 +369,6 @@ void BitparSolver::batch_impl(int64_t k0, int64_t nb, const int64_t* qoff, const
                               int64_t* Fout, int64_t* edges2, RunStats* st, hipStream_t s) {
   Loop S;
   S.cnt = n_eff();
-  S.cum_ok = true;  // (every level of the batch runs here and counts into Small::cum)
   // lazy: no per-batch fill of vis_[0] (n_eff * 8W bytes, ~0.8 ms on RMAT-26); the edge-counting
   // pass re-reads both rows of every new vertex (k_count_frontier), so it keeps the fill
   S.lazy = tun_.lazy && !COUNT && !fused_batches<COUNT>();

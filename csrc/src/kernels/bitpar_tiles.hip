@@ -150,8 +150,7 @@ const BitparSolver::TileSet* BitparSolver::pfx_tiles(int W, int part, int nparts
 
 // phase A of part `part` of `nparts` pulls its level 2 over the tiles of its own vertices
 void BitparSolver::prepare_hybrid(int part, int nparts, hipStream_t s) {
-  if (g_.rows_sorted && g_.n <= INT32_MAX && tun_.pfx == 2 && maxW_ >= 8)
-    (void)pfx_tiles(maxW_, part, nparts, s);
+  if (tiles_possible()) (void)pfx_tiles(maxW_, part, nparts, s);
   MSBFS_HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -165,8 +164,9 @@ void BitparSolver::hybrid_chunk_bounds(int part, int nparts, int64_t n_eff, int 
                                        int64_t* b, hipStream_t s) {
   if (chunks < 1) fail("hybrid: chunks must be >= 1");
   const int64_t cnt = n_eff > part ? (n_eff - part + nparts - 1) / nparts : 0;
-  const TileSet* T = (g_.rows_sorted && g_.n <= INT32_MAX && tun_.pfx == 2 && maxW_ >= 8)
-                         ? pfx_tiles(maxW_, part, nparts, s) : nullptr;
+  // (tile-aligned whenever any word count of this solver can take the tiled level: the tiles
+  // are the same for every word count, and an untiled level packs its ranges afterwards)
+  const TileSet* T = tiles_possible() ? pfx_tiles(maxW_, part, nparts, s) : nullptr;
   if (!T || T->ti.empty() || T->ti.back() != cnt) {
     for (int c = 0; c <= chunks; ++c) b[c] = cnt * c / chunks;
     return;
@@ -216,8 +216,13 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
   auto tile_at = [&](int c) -> int64_t {  // first tile of range c
     if (c <= 0) return 0;
     if (c >= nch) return T->ntiles;
-    return std::lower_bound(T->ti.begin(), T->ti.end() - 1, S.chunk_b[(size_t)c]) -
-           T->ti.begin();
+    const int64_t t = std::lower_bound(T->ti.begin(), T->ti.end() - 1, S.chunk_b[(size_t)c]) -
+                      T->ti.begin();
+    // a range must start at a tile start: a tile straddling two ranges would be computed by the
+    // launch of the earlier range, after the later range's piece had already left
+    if (T->ti[(size_t)t] != S.chunk_b[(size_t)c] || (c == 1 && t <= T->last_partial))
+      fail("tiled pull: exchange range " + std::to_string(c) + " does not start at a tile");
+    return t;
   };
   // ranges from the last (low-degree end) to the first (hubs): pieces go out in the order
   // their words are packed and the low-degree ranges hold most own vertices, i.e. most bytes

@@ -15,6 +15,7 @@ MI355X design:
 """
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
@@ -44,6 +45,14 @@ class DistContext:
         return torch.device("cuda", self.device) if self.device >= 0 else torch.device("cpu")
 
 
+def pg_timeout_s() -> float:
+    """Collective timeout of the process group: MSBFS_PG_TIMEOUT seconds (default 180)."""
+    t = float(os.environ.get("MSBFS_PG_TIMEOUT", "180"))
+    if not t > 0:
+        raise ValueError(f"MSBFS_PG_TIMEOUT must be > 0, got {t}")
+    return t
+
+
 def init_from_env(backend: Optional[str] = None, gpus_per_node: Optional[int] = None,
                   use_gpu: Optional[bool] = None) -> DistContext:
     """Initialise from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
@@ -71,7 +80,9 @@ def init_from_env(backend: Optional[str] = None, gpus_per_node: Optional[int] = 
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29500")
-            kw = {}
+            # a hung or mismatched collective fails loudly after pg_timeout_s, well inside the
+            # driver's lease, instead of blocking until the lease is killed
+            kw = {"timeout": datetime.timedelta(seconds=pg_timeout_s())}
             if backend == "nccl" and device >= 0:
                 kw["device_id"] = torch.device("cuda", device)
             dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
@@ -232,7 +243,7 @@ def allreduce_sum_i64(a: np.ndarray, ctx: DistContext) -> np.ndarray:
 
 
 def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistContext,
-                  stream=None) -> Tuple[int, int]:
+                  force_two_pass: bool = False) -> Tuple[int, int]:
     """Global (minK, minF) with the reference tie-break. (-1, -1) when K == 0 (main.cu:379-380).
 
     ONE all-reduce(MIN) of an int64 key 1 + (F << qbits | q). A rank whose F is too large to share
@@ -253,8 +264,9 @@ def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistC
 
     maxF = int(F_local.max()) if len(F_local) else 0
     fits = qb < 62 and (maxF >> (62 - qb)) == 0
-    key = allmin((1 + int(((F_local << qb) | idx_local).min()) if len(F_local) else NONE)
-                 if fits else 0)
+    key = 0 if force_two_pass else \
+        allmin((1 + int(((F_local << qb) | idx_local).min()) if len(F_local) else NONE)
+               if fits else 0)
     if key == NONE:
         return -1, -1
     if key > 0:
@@ -266,6 +278,79 @@ def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistC
     cand = idx_local[F_local == mf]
     mk = allmin(int(cand.min()) if len(cand) else NONE)
     return mk, mf
+
+
+class AsyncArgmin:
+    """packed_argmin in two halves: start() posts the step's 8-byte MIN all-reduce and returns at
+    once; wait() gives (minK, minF). Between the two the next step's BFS runs (bench.py waits
+    for step i's key after enqueueing step i + 1), so the reduction stays off the critical path.
+
+    Under RCCL the key goes H2D, through the all-reduce and back D2H on a side stream of its own
+    (non-blocking, never ordered against the solver's null-stream kernels). Two slots of pinned
+    and device buffers alternate, so a new start() never rewrites a key still in flight. Under
+    gloo it is an async host all-reduce. The reference runs MPI_Gather + MPI_Gatherv + a serial
+    scan on rank 0 after all compute (main.cu:340-397).
+    """
+
+    def __init__(self, ctx: DistContext):
+        self.ctx = ctx
+        self.slot = 0
+        self._bufs = None
+        self._stream = None
+
+    def start(self, F_local: np.ndarray, idx_local: np.ndarray, K: int):
+        import torch
+        import torch.distributed as dist
+
+        F_local = np.asarray(F_local, dtype=np.int64)
+        idx_local = np.asarray(idx_local, dtype=np.int64)
+        qb = _qbits(K)
+        NONE = np.iinfo(np.int64).max
+        maxF = int(F_local.max()) if len(F_local) else 0
+        fits = qb < 62 and (maxF >> (62 - qb)) == 0
+        key = ((1 + int(((F_local << qb) | idx_local).min())) if len(F_local) else NONE) \
+            if fits else 0
+        pend = {"F": F_local, "idx": idx_local, "K": K, "qb": qb, "key": key}
+        if not self.ctx.distributed:
+            return pend
+        dev = _comm_device(self.ctx)
+        if dev.type != "cuda":
+            t = torch.tensor([key], dtype=torch.int64)
+            pend["work"] = dist.all_reduce(t, op=dist.ReduceOp.MIN, async_op=True)
+            pend["t"] = t
+            return pend
+        if self._bufs is None:
+            self._bufs = [(torch.empty(1, dtype=torch.int64, pin_memory=True),
+                           torch.empty(1, dtype=torch.int64, device=dev)) for _ in range(2)]
+            self._stream = torch.cuda.Stream(device=dev)
+        h, d = self._bufs[self.slot]
+        self.slot ^= 1
+        h.numpy()[0] = key
+        with torch.cuda.stream(self._stream):
+            d.copy_(h, non_blocking=True)
+            dist.all_reduce(d, op=dist.ReduceOp.MIN)
+            h.copy_(d, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        pend["event"], pend["h"] = ev, h
+        return pend
+
+    def wait(self, pend) -> Tuple[int, int]:
+        NONE = np.iinfo(np.int64).max
+        key = pend["key"]
+        if "event" in pend:
+            pend["event"].synchronize()
+            key = int(pend["h"].numpy()[0])
+        elif "work" in pend:
+            pend["work"].wait()
+            key = int(pend["t"].numpy()[0])
+        if key == NONE:
+            return -1, -1
+        if key > 0:
+            key -= 1
+            return int(key & ((1 << pend["qb"]) - 1)), int(key >> pend["qb"])
+        # some rank's F does not fit next to the index: the two-pass form (every rank gets here)
+        return packed_argmin(pend["F"], pend["idx"], pend["K"], self.ctx, force_two_pass=True)
 
 
 def gather_F(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistContext) -> np.ndarray:

@@ -190,6 +190,87 @@ def chunk_views(send, recv, cnt: int, wbeg: np.ndarray, rank: int, pcounts, boun
     return ins, outs
 
 
+class PieceExchange:
+    """The overlapped exchange's pieces as point-to-point operations, one batch per piece.
+
+    Piece c sends to every peer j its words of this rank's own-vertex range c and receives
+    from every peer r its range c (chunk_views). Each piece is one dist.batch_isend_irecv:
+    grouped ncclSend/ncclRecv on RCCL's stream, or tagged isend/irecv under gloo. The local
+    block is a copy on the current stream. Both backends issue the same calls in the same
+    order, so the gloo tests run the sequence that the RCCL runs use. Gloo stages through host
+    memory: a send is copied to the host when its piece starts, and a receive lands in a host
+    buffer that finish() copies into recv.
+
+    Pairing rule: every rank starts every piece, in the same order. Piece c's sizes depend
+    only on the bounds agreed at setup, so a sender and its receiver agree on every size. A
+    piece that is empty on both sides issues no operation. The reference gathers with blocking
+    MPI_Gather + MPI_Gatherv after all compute (main.cu:340-365).
+    """
+
+    def __init__(self, ctx: D.DistContext, send, recv, cnt: int, wbeg: np.ndarray, pcounts,
+                 bounds: np.ndarray, chunks: int):
+        self.ctx, self.send, self.recv, self.cnt = ctx, send, recv, int(cnt)
+        self.wbeg, self.pcounts, self.bounds, self.chunks = wbeg, pcounts, bounds, int(chunks)
+        self.staged = ctx.distributed and ctx.backend != "nccl"
+        self.reset()
+
+    def reset(self) -> None:
+        self.works, self.landing, self.started = [], [], []
+
+    def order(self):
+        """Issue order of the pieces: last range first (the tiled pull's order, tiles_pull)."""
+        return list(range(self.chunks - 1, -1, -1))
+
+    def start(self, c: int) -> None:
+        import torch
+        import torch.distributed as dist
+
+        if c in self.started:
+            raise RuntimeError(f"exchange piece {c} started twice")
+        ctx = self.ctx
+        ins, outs = chunk_views(self.send, self.recv, self.cnt, self.wbeg, ctx.rank,
+                                self.pcounts, self.bounds, c)
+        self.started.append(c)
+        me = ctx.rank
+        if outs[me].numel():
+            outs[me].copy_(ins[me])
+        if not ctx.distributed:
+            return
+        ops = []
+        for j in range(ctx.world):
+            if j == me:
+                continue
+            if ins[j].numel():
+                ops.append(dist.P2POp(dist.isend, ins[j].cpu() if self.staged else ins[j], j,
+                                      tag=c))
+            if outs[j].numel():
+                dst = outs[j]
+                if self.staged:
+                    dst = torch.empty(outs[j].numel(), dtype=outs[j].dtype)
+                    self.landing.append((outs[j], dst))
+                ops.append(dist.P2POp(dist.irecv, dst, j, tag=c))
+        if ops:
+            self.works.extend(dist.batch_isend_irecv(ops))
+
+    def start_missing(self) -> None:
+        """Start every piece not started yet, in issue order (after a failure partway through
+        phase A: the peers still pair their calls with this rank's)."""
+        for c in self.order():
+            if c not in self.started:
+                self.start(c)
+
+    def finish(self) -> None:
+        """Wait for every piece. The received words are then visible to the current stream,
+        which the native kernels use too."""
+        for w in self.works:
+            w.wait()
+        for dst, src in self.landing:
+            dst.copy_(src)
+        if self.recv.is_cuda:
+            torch_sync(self.recv.device)
+        self.reset()
+
+
 class HybridRunner:
     """Reusable buffers + plan for one (solver, K, world) combination."""
 
@@ -219,18 +300,21 @@ class HybridRunner:
         self._staged = ctx.distributed and ctx.backend != "nccl"
         self.last_bytes = (0, 0)  # (sent, received) of the last exchange
         solver.prepare_hybrid(ctx.rank, ctx.world)  # (phase A's tables, outside timed runs)
-        # overlapped exchange: device collectives (RCCL) and the dense layout only (gloo stages
-        # through host memory, the coded segments exist only once the whole phase A is done)
+        # overlapped exchange: the dense layout only (the coded segments exist only once the
+        # whole phase A is done). Point-to-point pieces (PieceExchange): RCCL and gloo alike.
         if chunks is None:
-            chunks = DEFAULT_CHUNKS if (ctx.distributed and not self._staged and not self.coded) else 1
-        self.chunks = max(1, int(chunks)) if not (self.coded or self._staged) else 1
+            chunks = DEFAULT_CHUNKS if (ctx.distributed and not self.coded) else 1
+        self.chunks = max(1, int(chunks)) if not self.coded else 1
         self.pcounts = [part_count(self.n_eff, r, ctx.world) for r in range(ctx.world)]
         self.bounds = None
+        self.exchange = None
         if self.chunks > 1:
             b = solver.hybrid_chunk_bounds(ctx.rank, ctx.world, self.n_eff, self.chunks)
             full = np.zeros((ctx.world, self.chunks + 1), dtype=np.int64)
             full[ctx.rank] = b
             self.bounds = D.allreduce_sum_i64(full.reshape(-1), ctx).reshape(ctx.world, -1)
+            self.exchange = PieceExchange(ctx, self.send, self.recv, self.pcounts[ctx.rank],
+                                          self.wbeg, self.pcounts, self.bounds, self.chunks)
 
     def _all_to_all(self, recv, send, rsz, ssz) -> None:
         import torch
@@ -274,23 +358,28 @@ class HybridRunner:
             return D.checked(fn, ctx, what) if checked else fn()
 
         t0 = time.perf_counter()
-        works = []
         if self.chunks > 1:
-            cnt = self.pcounts[ctx.rank]
-
-            def on_chunk(c, i0, i1):  # starts piece c on the collective's stream (async)
-                ins, outs = chunk_views(self.send, self.recv, cnt, self.wbeg, ctx.rank,
-                                        self.pcounts, self.bounds, c)
-                if ctx.distributed:
-                    import torch.distributed as dist
-                    works.append(dist.all_to_all(outs, ins, async_op=True))
-                else:
-                    for o, x in zip(outs, ins):
-                        o.copy_(x)
-
-            out, sa = local(lambda: self.solver.hybrid_phase_a_chunked(
-                queries, ctx.rank, P, self.n_eff, ctx.rank == 0, self.wbeg,
-                self.send.data_ptr(), self.chunks, on_chunk), "hybrid phase A")
+            ex = self.exchange
+            ex.reset()
+            err = None
+            try:  # piece c starts as soon as phase A has packed range c (async)
+                out, sa = self.solver.hybrid_phase_a_chunked(
+                    queries, ctx.rank, P, self.n_eff, ctx.rank == 0, self.wbeg,
+                    self.send.data_ptr(), self.chunks, lambda c, i0, i1: ex.start(c))
+            except Exception as e:  # noqa: BLE001
+                err = e
+            if checked:
+                # a failure partway: still start the remaining pieces (their words are junk), so
+                # every peer's calls pair up, then fail on every rank together
+                if err is not None:
+                    ex.start_missing()
+                if not D.agree_ok(err is None, ctx):
+                    ex.finish()
+                    if err is not None:
+                        raise err
+                    raise RuntimeError("hybrid phase A failed on another rank")
+            elif err is not None:
+                raise err
         else:
             out, sa = local(lambda: self.solver.hybrid_phase_a(
                 queries, ctx.rank, P, self.n_eff, ctx.rank == 0, self.wbeg, self.send.data_ptr(),
@@ -311,10 +400,7 @@ class HybridRunner:
         elif self.chunks > 1:
             ssz, rsz = self.send_sizes, self.recv_sizes
             reduced = self._allreduce(out.copy())
-            for w in works:  # (the pieces started during phase A)
-                w.wait()
-            if self.recv.is_cuda:
-                torch_sync(self.recv.device)
+            self.exchange.finish()  # (the pieces started during phase A)
         else:
             ssz, rsz = self.send_sizes, self.recv_sizes
             reduced = self._allreduce(out.copy())

@@ -76,7 +76,8 @@ def test_bench_graph_two_ranks_gloo(msbfs_pkg):
     assert js["traversed_edges"] == int(ref.edges.sum())
 
 
-@pytest.mark.parametrize("ranks,dist", [(2, "hybrid"), (2, "hybrid-coded"), (3, "auto")])
+@pytest.mark.parametrize("ranks,dist", [(2, "hybrid"), (3, "hybrid"), (2, "hybrid-coded"),
+                                        (3, "auto")])
 def test_bench_multi_rank_gloo_shared_gpu(ranks, dist):
     """bench.py with several ranks on the one GPU (gloo collectives, the hybrid exchange staged
     through host memory): every rank runs its own solver, the hybrid phases exchange real
@@ -98,6 +99,8 @@ def test_bench_multi_rank_gloo_shared_gpu(ranks, dist):
         ph = cfg["phases"]  # per-phase wall ms (max over ranks) and the exchange rate
         assert ph["phase_a_wall_ms"] > 0 and ph["phase_c_wall_ms"] > 0 and ph["exchange_ms"] > 0
         assert ph["alltoall_GBps_per_rank"] is None or ph["alltoall_GBps_per_rank"] > 0
+        # the dense exchange overlaps phase A in point-to-point pieces under gloo too
+        assert ph["chunks"] == (1 if dist == "hybrid-coded" else 8)
     else:
         assert set(cfg["candidates_ms"]) == {"roundrobin", "hybrid", "hybrid-coded"}
 

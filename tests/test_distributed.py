@@ -78,7 +78,8 @@ def _argmin_worker(rank, world, port, out_dir):
     ctx = D.init_from_env(backend="gloo", use_gpu=False)
     K = 6
     F = np.array([9, 4, 2 ** 61, 4, 7, 4], np.int64)  # ties at q = 1, 3, 5
-    res = []
+    res, pend = [], []
+    amin = D.AsyncArgmin(ctx)
     for case in ("fit", "mixed", "empty-rank"):
         idx = D.round_robin(K, rank, world)
         Fl = F[idx].copy()
@@ -87,15 +88,35 @@ def _argmin_worker(rank, world, port, out_dir):
         if case == "empty-rank" and rank == 1:
             idx, Fl = idx[:0], Fl[:0]
         res.append(D.packed_argmin(Fl, idx, K, ctx))
+        pend.append(amin.start(Fl, idx, K))  # (several keys in flight at once)
+    res += [amin.wait(p) for p in pend]
     np.save(os.path.join(out_dir, f"a{rank}.npy"), np.array(res, np.int64))
     D.shutdown(ctx)
 
 
 def test_packed_argmin_gloo_mixed_fallback(tmp_path):
     """One rank's F too large to pack: every rank must take the fallback together (one MIN
-    all-reduce decides it) and agree on the reference's lowest-index tie-break."""
+    all-reduce decides it) and agree on the reference's lowest-index tie-break. The async form
+    (AsyncArgmin, bench.py's timed loop) gives the same answers with several keys in flight."""
     mp.spawn(_argmin_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     for r in range(2):
         got = [tuple(x) for x in np.load(tmp_path / f"a{r}.npy")]
         # rank 0 holds q = 0, 2, 4; rank 1 holds q = 1, 3, 5 (round robin)
-        assert got == [(1, 4), (1, 4), (4, 7)], got
+        assert got == [(1, 4), (1, 4), (4, 7)] * 2, got
+
+
+def test_async_argmin_single_process_and_pg_timeout(monkeypatch):
+    from msbfs.parallel import distributed as D
+    amin = D.AsyncArgmin(D.DistContext())
+    p = amin.start(np.array([5, 3, 3, 9]), np.array([0, 1, 2, 3]), 4)
+    assert amin.wait(p) == (1, 3)
+    p = amin.start(np.array([2 ** 61, 2 ** 61]), np.array([7, 3]), 8)
+    assert amin.wait(p) == (3, 2 ** 61)
+    assert amin.wait(amin.start(np.array([], np.int64), np.array([], np.int64), 0)) == (-1, -1)
+    monkeypatch.delenv("MSBFS_PG_TIMEOUT", raising=False)
+    assert D.pg_timeout_s() == 180
+    monkeypatch.setenv("MSBFS_PG_TIMEOUT", "30")
+    assert D.pg_timeout_s() == 30
+    monkeypatch.setenv("MSBFS_PG_TIMEOUT", "0")
+    with pytest.raises(ValueError):
+        D.pg_timeout_s()

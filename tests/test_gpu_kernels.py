@@ -299,8 +299,8 @@ def test_bitpar_tiled_first_pull(msbfs_pkg, K):
             "fewcodes": {"tiles_code_deg": 1}, "manycodes": {"tiles_code_deg": 400},
             "td3": {"dirs": "TBT"}, "td3plain": {"dirs": "TBT", "tiles": 0},
             "pushbefore": {"push_after": 0}, "td3pushbefore": {"dirs": "TBT", "push_after": 0},
-            "pushafter_nocodes": {"push_after": 1, "codes": 0}, "hskip": {"hskip": 1},
-            "hskip_nolean": {"hskip": 1, "lean_min": 1 << 40}, "chunk2": {"chunk2": 1},
+            "pushafter_nocodes": {"push_after": 1, "codes": 0}, "chunk2": {"chunk2": 1},
+            "nolean": {"lean_min": 1 << 40},
             # tiles from 4 words on (K = 200: W = 4, no codes there)
             "tiles4": {"tiles_w": 4}, "tiles4_pushbefore": {"tiles_w": 4, "push_after": 0},
             "td3tiles4": {"dirs": "TBT", "tiles_w": 4}}
@@ -615,10 +615,7 @@ def test_dist_device_batches_and_reset(msbfs_pkg):
 
 @pytest.mark.parametrize("dirs", ["", "TBBTBBTBBTBBTBBT", "TBTBTBTBTBTBTBTB", "TBBBBBBBBBBBBBBT"])
 @pytest.mark.parametrize("extra", [{}, {"lean_min": 0}, {"bu_max": 1 << 30}, {"full": 0},
-                                   {"lean_min": 0, "first_u": 2},
-                                   {"lean_min": 0, "first_u": 4, "lean_level": 2},
-                                   {"dskip3": 0}, {"hskip": 1}, {"hskip": 1, "lean_min": 0},
-                                   {"hskip": 1, "bu_max": 1 << 30}])
+                                   {"dskip3": 0}])
 def test_bitpar_done_rows_skipped(msbfs_pkg, dirs, extra):
     """dskip (round 4): unfiltered pull levels never read done vertices' rows (a level-start
     snapshot of the done bitmap is probed, the alive mask ORed) and write none for the vertices
