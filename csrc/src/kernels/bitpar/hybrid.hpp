@@ -252,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
                                                          const uint64_t* gmask, uint32_t* done,
                                                          uint32_t* anyvis, const int64_t* rowptr,
                                                          int wide_deg, int32_t* act,
-                                                         int32_t* actw, Ctr* ctr) {
+                                                         int32_t* actw, Ctr* ctr, int pshift) {
   // G lanes per vertex (the solver's row layout): every row read and write is coalesced (with one
   // thread per vertex the W-word rows were written at a W*8-byte lane stride: 6.9 ms instead of
   // ~1 ms at W = 8). A block covers TILE consecutive vertices, a multiple of 32, so it writes whole
@@ -277,7 +277,10 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
     V<VW> x = vzero<VW>();
     int64_t deg = 0;
     if (v < n_eff) {
-      const uint64_t* src = recv + (pre.b[v % nparts] + v / nparts) * nw;
+      // (a power-of-two part count splits v with a mask and a shift, not a 64-bit division)
+      const int64_t part = pshift >= 0 ? (v & (nparts - 1)) : v % nparts;
+      const int64_t idx = pshift >= 0 ? (v >> pshift) : v / nparts;
+      const uint64_t* src = recv + (pre.b[part] + idx) * nw;
       if (slot == 0) deg = rowptr[v + 1] - rowptr[v];
 #pragma unroll
       for (int j = 0; j < VW; ++j) {

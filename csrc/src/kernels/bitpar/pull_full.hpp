@@ -116,8 +116,21 @@ __device__ __forceinline__ void wq_flush_block(int32_t* q, uint32_t& n, int32_t*
 // four waves per SIMD, and the pull is latency-bound there).
 template <int W>
 constexpr int full_cs() { return W <= 4 ? 4 : 8; }
+// (experiment knobs, round 5: occupancy / queue size / counter slices of the W >= 4 pulls)
+#ifndef MSBFS_FULL_OCC
+#define MSBFS_FULL_OCC 4
+#endif
+#ifndef MSBFS_FULL_Q
+#define MSBFS_FULL_Q 1024
+#endif
+#ifndef MSBFS_FULL_SL
+#define MSBFS_FULL_SL 7
+#endif
+#ifndef MSBFS_FULL_PF
+#define MSBFS_FULL_PF 1
+#endif
 template <int W, int CS = full_cs<W>(), int C1 = 0>
-__global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
+__global__ __launch_bounds__(kBlock, W <= 2 ? 5 : MSBFS_FULL_OCC) void k_bu_full(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, int64_t n, const uint64_t* alive, const uint64_t* gmask,
     uint32_t* done, int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* actw2,
@@ -125,6 +138,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
     const uint32_t* dsnap, int flags) {
   if (!bu_gate_open(gate)) return;  // (uniform)
   const bool skip = flags & kFlagSkipRows;
+  constexpr bool PF = MSBFS_FULL_PF == 2 || (MSBFS_FULL_PF == 1 && W >= 4);
   if (nact_dev) nact = (int64_t)*nact_dev;
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
@@ -138,7 +152,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   // another tile's pushes might not fit; 1024-item queues keep them at about the round-3 block
   // queues' count (448-item ones made level 3 pay ~170K of them) and fill the LDS of four
   // blocks per CU (the VGPR bound) exactly (768 for up to 2 words: five blocks per CU).
-  constexpr int QA = W <= 2 ? 768 : 1024, QF = QA, QW = 2 * VPW > 128 ? 2 * VPW : 128;
+  constexpr int QA = W <= 2 ? 768 : MSBFS_FULL_Q, QF = QA, QW = 2 * VPW > 128 ? 2 * VPW : 128;
   static_assert(QW >= 2 * VPW, "a wide push always fits after a flush");
   __shared__ int32_t qmem[kWaves][QA + QF + QW];
   __shared__ unsigned long long scratch[kWaves];
@@ -165,7 +179,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   // 32-bit halves (~12 VALU per set counter bit instead of ~28: level 3 spills find most
   // counter bits set, ~50 VALU per tile with 6 slices and 64-bit spills); 5 slices for few
   // words (one spill every 31 tiles, the 96-VGPR bound)
-  BitCounter<VW, W <= 4 ? 5 : (W >= 16 ? 7 : 6)> bc;
+  BitCounter<VW, W <= 4 ? 5 : (W >= 16 ? MSBFS_FULL_SL : 6)> bc;
   bc.zero();
   int nadd = 0;
   // software pipeline (as k_bu_narrow): list entry two tiles ahead, own row / offsets one tile
@@ -205,6 +219,16 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
       }
     }
   };
+  // column entries [e, e + C) of a row ending at `end`: slot q*G + lane's entry, -1 past the end
+  auto step_ids = [&](int64_t e, int64_t end, int32_t (&u)[Q]) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int64_t ee = e + q * G + slot;
+      const int32_t x = col[ee < end ? ee : 0];
+      u[q] = ee < end ? x : -1;
+    }
+  };
+  int32_t un[Q];    // ids of the group's next continuation step (MSBFS_FULL_PF)
   int32_t u1[Q];
   uint32_t pd1[Q];  // dsnap words of u1 (the done probe, loaded a tile ahead too)
   first_ids(b1, e1, u1);
@@ -277,6 +301,9 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
         // flight; their offsets were loaded at the top of this tile)
         if (v1 < 0) e1 = b1;
         first_ids(b1, e1, u1);
+        // and the ids of this vertex's second step: a group the first step leaves open issues
+        // its next rows without another round trip for the column ids
+        if (PF) step_ids(beg + F1, end, un);
         bool cov = true;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
@@ -288,11 +315,12 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
       }
       for (int64_t e = beg + F1; g_open && e < end; e += C) {
         int32_t u[Q];
+        if (PF) {  // (loaded one step ahead; the next step's now)
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          const int64_t ee = e + q * G + slot;
-          const int32_t x = col[ee < end ? ee : e];
-          u[q] = ee < end ? x : -1;
+          for (int q = 0; q < Q; ++q) u[q] = un[q];
+          step_ids(e + C, end, un);
+        } else {
+          step_ids(e, end, u);
         }
         if (dsnap) {
           uint32_t pd[Q];

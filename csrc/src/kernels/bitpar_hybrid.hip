@@ -241,7 +241,8 @@ void BitparSolver::phase_c_impl(int64_t K, int w_begin, int w_count, int nparts,
       }
     MSBFS_HIP_CHECK(hipMemcpyAsync(sm.alive[0], ha, 16 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     MSBFS_HIP_CHECK(hipMemcpyAsync(sm.gmask, ha + 16, 16 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    MSBFS_HIP_CHECK(hipStreamSynchronize(s));
+    // (no wait here: the read_ctr after k_hybrid_setup retires these copies before hsrc_ is
+    // written again)
   }
   if (n_eff > 0) {  // vertices >= n_eff have no edges: no kernel reads their rows or bits
     PartPrefix pre{};
@@ -250,7 +251,7 @@ void BitparSolver::phase_c_impl(int64_t K, int w_begin, int w_count, int nparts,
         recv, w_count, n_eff, nparts, pre, vis_[0].as<uint64_t>(), vis_[1].as<uint64_t>(),
         sm.alive[0], sm.gmask, done_.as<uint32_t>(), anyvis_.as<uint32_t>(), g_.rowptr,
         std::max(opt.wide_degree, kWideLater), act_[0].as<int32_t>(), actw_[0].as<int32_t>(),
-        ctr_.as<Ctr>());
+        ctr_.as<Ctr>(), (nparts & (nparts - 1)) == 0 ? __builtin_ctz((unsigned)nparts) : -1);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   Loop S;

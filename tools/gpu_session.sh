@@ -46,6 +46,14 @@ for s in "$@"; do
     road16) step road16 900 python tools/bench_graph.py --graph grid:4896:4896:0.6 --groups 16 --steps 1 ;;
     profroad) prof profroad 900 python tools/bench_graph.py --graph grid:4896:4896:0.6 --groups 64 --steps 1 ;;
     uniform) step uniform 600 python tools/bench_graph.py --graph uniform:16000000:128000000 --groups 1024 --steps 3 ;;
+    exitrt)  # teardown under the runtime tracer, least to most state (stops at the first crash)
+      export TMPDIR=/tmp
+      for m in load device solve leak bench; do
+        if [ $m = bench ]; then cmd="python bench.py --steps 2 --warmup 1 --verify 0"
+        else cmd="python tools/exit_check.py $m"; fi
+        step exitrt_$m 300 rocprofv3 --runtime-trace --output-format csv -d gpurun_out/exrt_$m \
+          -o run -- $cmd
+      done ;;
     hybsim) step hybsim 900 python tools/hybrid_sim.py --scale 26 --ranks 2 4 8 ;;
     hybsim8) step hybsim8 600 python tools/hybrid_sim.py --scale 26 --ranks 8 --no-roundrobin ;;
     profhyb8) prof profhyb 900 python tools/hybrid_sim.py --scale 26 --ranks 8 --no-roundrobin ;;
