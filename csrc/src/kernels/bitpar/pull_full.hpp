@@ -116,21 +116,11 @@ __device__ __forceinline__ void wq_flush_block(int32_t* q, uint32_t& n, int32_t*
 // four waves per SIMD, and the pull is latency-bound there).
 template <int W>
 constexpr int full_cs() { return W <= 4 ? 4 : 8; }
-// (experiment knobs, round 5: occupancy / queue size / counter slices of the W >= 4 pulls)
-#ifndef MSBFS_FULL_OCC
-#define MSBFS_FULL_OCC 4
-#endif
-#ifndef MSBFS_FULL_Q
-#define MSBFS_FULL_Q 1024
-#endif
-#ifndef MSBFS_FULL_SL
-#define MSBFS_FULL_SL 7
-#endif
-#ifndef MSBFS_FULL_PF
-#define MSBFS_FULL_PF 1
-#endif
+// PF: a step loads the column ids of the group's next step (from 4 words on; at 1-2 words the
+// extra ids spilled registers). RMAT-26 / 1024 groups level 3: 5.30 -> 5.19 ms (round 5). (Five
+// waves per SIMD with 512-entry queues spilled 37-47 VGPRs at 16 words: not kept.)
 template <int W, int CS = full_cs<W>(), int C1 = 0>
-__global__ __launch_bounds__(kBlock, W <= 2 ? 5 : MSBFS_FULL_OCC) void k_bu_full(
+__global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, int64_t n, const uint64_t* alive, const uint64_t* gmask,
     uint32_t* done, int32_t* act2, int32_t* fl2, Ctr* ctr, uint32_t* anyvis, int32_t* actw2,
@@ -138,7 +128,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : MSBFS_FULL_OCC) void k_bu_full
     const uint32_t* dsnap, int flags) {
   if (!bu_gate_open(gate)) return;  // (uniform)
   const bool skip = flags & kFlagSkipRows;
-  constexpr bool PF = MSBFS_FULL_PF == 2 || (MSBFS_FULL_PF == 1 && W >= 4);
+  constexpr bool PF = W >= 4;
   if (nact_dev) nact = (int64_t)*nact_dev;
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
@@ -152,7 +142,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : MSBFS_FULL_OCC) void k_bu_full
   // another tile's pushes might not fit; 1024-item queues keep them at about the round-3 block
   // queues' count (448-item ones made level 3 pay ~170K of them) and fill the LDS of four
   // blocks per CU (the VGPR bound) exactly (768 for up to 2 words: five blocks per CU).
-  constexpr int QA = W <= 2 ? 768 : MSBFS_FULL_Q, QF = QA, QW = 2 * VPW > 128 ? 2 * VPW : 128;
+  constexpr int QA = W <= 2 ? 768 : 1024, QF = QA, QW = 2 * VPW > 128 ? 2 * VPW : 128;
   static_assert(QW >= 2 * VPW, "a wide push always fits after a flush");
   __shared__ int32_t qmem[kWaves][QA + QF + QW];
   __shared__ unsigned long long scratch[kWaves];
@@ -179,7 +169,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : MSBFS_FULL_OCC) void k_bu_full
   // 32-bit halves (~12 VALU per set counter bit instead of ~28: level 3 spills find most
   // counter bits set, ~50 VALU per tile with 6 slices and 64-bit spills); 5 slices for few
   // words (one spill every 31 tiles, the 96-VGPR bound)
-  BitCounter<VW, W <= 4 ? 5 : (W >= 16 ? MSBFS_FULL_SL : 6)> bc;
+  BitCounter<VW, W <= 4 ? 5 : (W >= 16 ? 7 : 6)> bc;
   bc.zero();
   int nadd = 0;
   // software pipeline (as k_bu_narrow): list entry two tiles ahead, own row / offsets one tile
@@ -228,7 +218,7 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : MSBFS_FULL_OCC) void k_bu_full
       u[q] = ee < end ? x : -1;
     }
   };
-  int32_t un[Q];    // ids of the group's next continuation step (MSBFS_FULL_PF)
+  int32_t un[Q];    // ids of the group's next continuation step (PF)
   int32_t u1[Q];
   uint32_t pd1[Q];  // dsnap words of u1 (the done probe, loaded a tile ahead too)
   first_ids(b1, e1, u1);

@@ -92,14 +92,6 @@ __global__ __launch_bounds__(256) void k_fill_pent(const PfxTile* tiles, int64_t
   }
 }
 
-// (timing experiment, round 5: bits of MSBFS_TSKIP drop one part of the kernel's work; results
-// are wrong with any bit set. 1 code ORs, 2 dense-row ORs, 4 dense-row loads, 8 output-row
-// stores, 16 group counters, 32 code loads)
-#ifndef MSBFS_TSKIP
-#define MSBFS_TSKIP 0
-#endif
-constexpr int kTSkip = MSBFS_TSKIP;
-
 // One round = up to kRound entries of one tile. Rounds are software-pipelined across the
 // wave's tiles (tile t, t + nwaves, ...): while round r is processed, the packed entries of
 // round r + 1 are in flight (the entry stream comes from HBM).
@@ -223,8 +215,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
       for (int q = 0; q < Q; ++q) {
         const uint32_t u = pk[q] & kPentUMask;
         const bool coded = pk[q] != kPentNone && (int32_t)u >= code_from;
-        const uint32_t c = (kTSkip & 32) ? (1u << 30) | (u & 1023u)
-                                         : code[coded ? u : (uint32_t)code_from];
+        const uint32_t c = code[coded ? u : (uint32_t)code_from];
         cd[q] = coded ? c : kDenseCode;
       }
     }
@@ -232,7 +223,6 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
   TileRound rc = tile_first_round(tiles, ntiles, (int64_t)blockIdx.x * NWV + wv);
   TileRound rb = tile_next_round(tiles, ntiles, nwaves, rc);  // (rc's successor)
   uint32_t pkc[Q], cdc[Q], pkb[Q];
-  uint64_t sink = 0;  // (MSBFS_TSKIP)
   load_round(rc, pkc);
   while (rc.t < ntiles) {
     load_round(rb, pkb);    // entries of round r + 1 in flight
@@ -254,8 +244,7 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
       for (int i = 0; i < kCodeSlots; ++i) {
         const uint32_t g = (cdc[q] >> (10 * i)) & 1023u;
         const bool on = coded && (uint32_t)i < nset;
-        if constexpr (kTSkip & 1) sink += on ? vrow + g : 0u;
-        else atomicOr(&y32[on ? vrow + (g >> 5) : 2 * dummy], 1u << (g & 31));
+        atomicOr(&y32[on ? vrow + (g >> 5) : 2 * dummy], 1u << (g & 31));
       }
       pkc[q] = coded ? kPentNone : pkc[q];
     }
@@ -283,21 +272,13 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
         const uint64_t* src = uu[q] != kPentNone
                                   ? R + (int64_t)(uu[q] & kPentUMask) * W + slot * VW
                                   : zrow + slot * VW;
-        if constexpr (kTSkip & 4) {
-          x[q].w[0] = (uint64_t)(uintptr_t)src;
-          if constexpr (VW == 2) x[q].w[1] = 0;
-        } else {
-          x[q] = ldv<VW>(src);
-        }
+        x[q] = ldv<VW>(src);
       }
 #pragma unroll
       for (int q = 0; q < PB; ++q) {
         const int base = uu[q] != kPentNone ? (int)(uu[q] >> kPentUBits) * W + slot * VW : -1;
 #pragma unroll
-        for (int j = 0; j < VW; ++j) {
-          if constexpr (kTSkip & 2) sink ^= x[q].w[j] + (uint64_t)base;
-          else atomicOr(&y[base >= 0 ? base + j : dummy], x[q].w[j]);
-        }
+        for (int j = 0; j < VW; ++j) atomicOr(&y[base >= 0 ? base + j : dummy], x[q].w[j]);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -391,16 +372,11 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
             notfull |= (unv & ~nw.w[j]) != 0;
             rnz |= r.w[j] != 0;
           }
-          if constexpr (kTSkip & 8) sink ^= nvr.w[0];
-          else if (put) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
-          if constexpr (kTSkip & 16) {
-            sink ^= nw.w[0];
-          } else {
-            bc.add(nw);
-            if (++nadd == (1 << decltype(bc)::D) - 1) {
-              bc.template spill_strided32<CR>(cnt, slot);
-              nadd = 0;
-            }
+          if (put) stv<VW>(O + (int64_t)v * W + slot * VW, nvr);
+          bc.add(nw);
+          if (++nadd == (1 << decltype(bc)::D) - 1) {
+            bc.template spill_strided32<CR>(cnt, slot);
+            nadd = 0;
           }
           // per-group flags (a group's lanes share validity; the others OR over its words),
           // compressed to one bit per group = per vertex of the pass
@@ -438,7 +414,6 @@ __global__ __launch_bounds__(kTileBlock, 1) void k_pfx_tiles(
     for (int q = 0; q < Q; ++q) pkc[q] = pkb[q];
   }
   bc.template spill_strided32<CR>(cnt, slot);
-  if (kTSkip && sink == 0x9E3779B97F4A7C15ull) cnt[lane] = 1;  // (keeps the sink alive)
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t a = 0;
