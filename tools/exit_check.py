@@ -9,6 +9,9 @@ MODE narrows down which teardown crashes:
   device  + create a device graph and free it
   solve   + one small bit-parallel solve (the smoke path), every handle closed before exit
   leak    the same solve, handles left to the interpreter's teardown
+  torch   import torch and initialise its HIP context only (no msbfs)
+  tsolve  torch's context, then the solve of `solve`
+  tbig    torch's context, an RMAT-24 device graph and a 1024-group solve (bench.py's shape)
 Each mode prints "exit_check MODE done" just before the interpreter exits; a crash after that
 line is a teardown crash.
 """
@@ -19,17 +22,28 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main(mode: str) -> int:
+    if mode.startswith("t"):
+        import torch
+        torch.cuda.init()
+        torch.cuda.synchronize(0)
+        if mode == "torch":
+            print(f"exit_check {mode} done", flush=True)
+            return 0
     import msbfs
     from msbfs.ops import native
     assert native.available()
-    if mode in ("device", "solve", "leak"):
-        g = msbfs.DeviceGraph.rmat(12, 16, 1, device=0)
-        if mode in ("solve", "leak"):
-            qs = msbfs.QuerySet.random(g.n, 100, 4, 7)
+    if mode in ("device", "solve", "leak", "tsolve", "tbig"):
+        big = mode == "tbig"
+        g = msbfs.DeviceGraph.rmat(24 if big else 12, 16, 1, device=0)
+        if big:
+            g.relabel_by_degree()
+        if mode != "device":
+            qs = msbfs.QuerySet.random(g.n, 1024 if big else 100, 16 if big else 4, 7)
             s = msbfs.Solver(g, "bitpar", max_groups=qs.K)
+            s.prepare()
             r = s.run(qs)
             print("F[0] =", int(r.F[0]))
-            if mode == "solve":
+            if mode != "leak":
                 s.close()
         if mode != "leak":
             g.close()

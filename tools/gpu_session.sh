@@ -48,7 +48,7 @@ for s in "$@"; do
     uniform) step uniform 600 python tools/bench_graph.py --graph uniform:16000000:128000000 --groups 1024 --steps 3 ;;
     exitrt)  # teardown under the runtime tracer, least to most state (stops at the first crash)
       export TMPDIR=/tmp
-      for m in load device solve leak bench; do
+      for m in ${EXIT_MODES:-torch tsolve tbig bench}; do
         if [ $m = bench ]; then cmd="python bench.py --steps 2 --warmup 1 --verify 0"
         else cmd="python tools/exit_check.py $m"; fi
         step exitrt_$m 300 rocprofv3 --runtime-trace --output-format csv -d gpurun_out/exrt_$m \
