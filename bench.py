@@ -91,21 +91,32 @@ def main() -> int:
         return 2
     metric = METRIC if args.scale == 26 else METRIC.replace("RMAT-26", f"RMAT-{args.scale}")
 
-    import torch
     import msbfs
+    from msbfs.ops import native
     from msbfs.parallel import distributed as D
     from msbfs.parallel import hybrid as H
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # (one process: no torch at all, see D.init_from_env; several ranks: torch.distributed)
     ctx = D.init_from_env(backend=args.backend, use_gpu=True)
     dev = ctx.device
+    if ctx.distributed:
+        import torch
+        import torch.distributed as tdist
+
+        def sync():
+            torch.cuda.synchronize(dev)
+        pg_size = tdist.get_world_size() if tdist.is_initialized() else 1
+        cur_dev = torch.cuda.current_device()
+    else:
+        def sync():
+            native.check(native.lib().msbfs_device_sync())
+        pg_size, cur_dev = 1, dev
     # which GPU every rank drives: one per rank under RCCL (it refuses duplicates anyway)
-    devices = D.allgather_int(torch.cuda.current_device(), ctx)
+    devices = D.allgather_int(cur_dev, ctx)
     if ctx.backend == "nccl" and ctx.world > 1 and len(set(devices)) != len(devices):
         print(f"bench: ranks share GPUs under RCCL: {devices}", file=sys.stderr)
         return 2
-    import torch.distributed as tdist
-    pg_size = tdist.get_world_size() if ctx.distributed and tdist.is_initialized() else 1
     t_setup = time.perf_counter()
     g = msbfs.DeviceGraph.rmat(args.scale, args.edgefactor, args.seed, device=dev)
     relabelled = False
@@ -151,7 +162,7 @@ def main() -> int:
     if "roundrobin" not in plans and args.dist in ("auto", "roundrobin"):
         print(f"bench: round robin could not be set up: {cand_err}", file=sys.stderr)
         return 3
-    torch.cuda.synchronize(dev)
+    sync()
     setup_s = time.perf_counter() - t_setup
 
     def step(m, checked=False):
@@ -189,7 +200,7 @@ def main() -> int:
 
     cand_ms, errs = D.evaluate_candidates(candidates, run_gathered, F_ref, ctx,
                                           reps=2 if ctx.distributed else 1,
-                                          sync=lambda: torch.cuda.synchronize(dev))
+                                          sync=sync)
     cand_err.update(errs)
     for m, e in errs.items():
         if ctx.rank == 0:
@@ -216,10 +227,10 @@ def main() -> int:
 
     run_steps(max(0, args.warmup))
     D.barrier(ctx)
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     F, stats, (min_k, min_f) = run_steps(args.steps)
-    torch.cuda.synchronize(dev)
+    sync()
     D.barrier(ctx)
     dt = time.perf_counter() - t0
     dt = D.allreduce_max(dt, ctx)  # slowest rank

@@ -245,6 +245,9 @@ int msbfs_graph_wrap_device(int device, int64_t n, int64_t nnz, int64_t* d_rowpt
                             msbfs_graph* out) {
   return guard([&] {
     MSBFS_HIP_CHECK(hipSetDevice(device));
+    // (the one-lane-per-vertex pulls read column ids as aligned 16-byte words)
+    if (reinterpret_cast<uintptr_t>(d_col) & 15)
+      msbfs::fail("graph wrap: the column array must be 16-byte aligned");
     auto h = std::make_unique<msbfs_graph_s>();
     h->g.device = device;
     h->g.n = n;

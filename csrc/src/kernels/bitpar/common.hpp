@@ -26,6 +26,26 @@ struct Lay {
   static constexpr uint64_t GBITS = (G == 64) ? ~0ull : ((1ull << G) - 1);
 };
 
+// One lane per vertex (G == 1): column entries [b, b + 4) of a row ending at e (-1 past it) from
+// two aligned 16-byte loads, i.e. one address per four entries instead of one per entry (the
+// address unit is the busy resource of these pulls). col must be 16-byte aligned (the graph
+// constructors check it); the second load re-reads the first window when the row ends before
+// it, and an aligned window never leaves the page of the valid entry it starts at.
+__device__ __forceinline__ void col4_aligned(const int32_t* col, int64_t b, int64_t e,
+                                             int32_t (&u)[4]) {
+  typedef int32_t i4 __attribute__((ext_vector_type(4)));
+  const int64_t a = b & ~(int64_t)3;
+  const int sh = (int)(b - a);
+  const i4 w0 = *(const i4*)(col + a);
+  const i4 w1 = *(const i4*)(col + (a + 4 < e ? a + 4 : a));
+  const int32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int32_t x = sh == 0 ? w[q] : sh == 1 ? w[q + 1] : sh == 2 ? w[q + 2] : w[q + 3];
+    u[q] = b + q < e ? x : -1;
+  }
+}
+
 template <int VW>
 struct V {
   uint64_t w[VW];

@@ -381,11 +381,21 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
     d1 = (uint32_t)(rowptr[v1 + 1] - b1);
     if constexpr (PFX) p1 = (uint32_t)plen[v1];
   }
+  // one lane per vertex, four-entry steps: aligned 16-byte id loads (col4_aligned, pull_full.hpp)
+  constexpr bool A4 = G == 1 && Q == 4 && C == 4;
   int32_t u1[Q];  // first-step column ids of the current tile's vertex (third pipeline stage)
+  auto first_ids = [&](bool ok, int32_t (&u)[Q]) {
+    if constexpr (A4) {
+      const int64_t n1 = ok ? (int64_t)(PFX ? p1 : d1) : 0;
+      col4_aligned(col, ok ? b1 : 0, ok ? b1 + n1 : 0, u);
+    } else {
 #pragma unroll
-  for (int q = 0; q < Q; ++q)
-    u1[q] = (tb + lofs < nact && q * G + slot < C && (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
-                ? col[b1 + q * G + slot] : -1;
+      for (int q = 0; q < Q; ++q)
+        u[q] = (ok && q * G + slot < C && (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
+                   ? col[b1 + q * G + slot] : -1;
+    }
+  };
+  first_ids(tb + lofs < nact, u1);
   for (; tb < nact; tb += stride) {
     const int64_t idx = tb + lofs;
     const bool valid = idx < nact;
@@ -447,12 +457,21 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
     if (g_open && !g_cov) {
       for (int64_t e = e0; e < end; e += C) {
         int32_t u[Q];
+        bool loaded = false;
+        if constexpr (A4) {
+          if (!(C1 == 0 && e == beg)) {
+            col4_aligned(col, e, end, u);
+            loaded = true;
+          }
+        }
+        if (!loaded) {
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          const int64_t ee = e + q * G + slot;
-          // first step: preloaded (without the short first step)
-          u[q] = (C1 == 0 && e == beg) ? u0[q]
-                                       : ((q * G + slot < C && ee < end) ? col[ee] : -1);
+          for (int q = 0; q < Q; ++q) {
+            const int64_t ee = e + q * G + slot;
+            // first step: preloaded (without the short first step)
+            u[q] = (C1 == 0 && e == beg) ? u0[q]
+                                         : ((q * G + slot < C && ee < end) ? col[ee] : -1);
+          }
         }
 
         // ids below filter_from are loaded without a probe (filter off: filter_from = INT_MAX)
@@ -530,11 +549,7 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
       if (leader && g_first) ev += deg;
     }
     // third stage: the next tile's first-step ids (its offsets arrived during this tile)
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-      u1[q] = (idx + stride < nact && q * G + slot < C &&
-               (uint32_t)(q * G + slot) < (PFX ? p1 : d1))
-                  ? col[b1 + q * G + slot] : -1;
+    first_ids(idx + stride < nact, u1);
     q_push(qa, keep && (int)deg <= next_wide, v);
     q_push(qw, keep && (int)deg > next_wide, v);
     q_push(qf, app, v);
@@ -865,6 +880,104 @@ __device__ __forceinline__ void chunk_pull(int32_t v, int64_t beg, int64_t lim, 
   }
 }
 
+// chunk_pull for the prefix-pull level without codes (fewer than 8 words, or codes off): every
+// id of a row prefix is below the LDS hub bitmap's bound, so the probes are LDS reads only, and
+// no chunk exits early (coop = 0 at the first pull level). The next tile's column ids are loaded
+// while the current tile is probed and gathered; every load is unconditional (clamped index,
+// result selected after), so the compiler waits for exactly the loads each use needs instead of
+// all of them (RMAT-30 / 32 groups: the level's chunk pulls stream ~10^10 prefix entries at one
+// word per vertex, and a wave otherwise waited for every tile's ids from HBM in turn).
+template <int W, int T, int HUBW>
+__device__ __forceinline__ void chunk_pull_pfx(int32_t v, int64_t beg, int64_t lim,
+                                               const int32_t* col, const uint64_t* R,
+                                               const V<Lay<W>::VW>& am, uint64_t* acc,
+                                               const uint32_t* hub, int32_t* lst,
+                                               const uint32_t* snap) {
+  static_assert(HUBW > 0, "the prefix chunks probe the LDS hub bitmap");
+  using L = Lay<W>;
+  constexpr int VW = L::VW, G = L::G, S = L::VPW;
+  constexpr int PB = VW == 2 ? 4 : 8;  // rows in flight per lane group in phase B
+  constexpr int Q = T / 64;
+  const int lane = lane_id(), slot = lane % G, sub = lane / G;
+  const int64_t vo = (int64_t)v * W + slot * VW;
+  const V<VW> r = (snap && !any_visited(snap, v)) ? vzero<VW>() : ldv<VW>(R + vo);
+  V<VW> unv, a = vzero<VW>();
+  bool lane_open = false;
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    unv.w[j] = ~r.w[j] & am.w[j];
+    lane_open |= unv.w[j] != 0;
+  }
+  if (!__ballot(lane_open)) return;  // wave-uniform
+  auto load_ids = [&](int64_t t0, int32_t (&u)[Q]) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int64_t e = t0 + q * 64 + lane;
+      const int32_t x = col[e < lim ? e : beg];
+      u[q] = e < lim ? x : -1;
+    }
+  };
+  int32_t un[Q];
+  load_ids(beg, un);
+  bool covered = false;
+  for (int64_t t0 = beg; t0 < lim && !covered; t0 += T) {
+    int32_t u[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) u[q] = un[q];
+    load_ids(t0 + T, un);  // (past the end: clamped, unused)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t h = hub[(u[q] >= 0 ? u[q] : 0) >> 5];
+      if (u[q] >= 0 && !((h >> (u[q] & 31)) & 1u)) u[q] = -1;
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint64_t m = __ballot(u[q] >= 0);
+      if (u[q] >= 0) lst[cnt + __popcll(m & lanemask_lt())] = u[q];
+      cnt += __popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int b = 0; b < cnt; b += PB * S) {
+      int32_t uu[PB];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int k = b + q * S + sub;
+        const int32_t x = lst[k < cnt ? k : 0];
+        uu[q] = k < cnt ? x : -1;
+      }
+      // (idle lanes load nothing: their address costs the address unit as much as a row)
+      V<VW> x[PB];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        x[q] = vzero<VW>();
+        if (uu[q] >= 0) x[q] = ldv<VW>(R + (int64_t)uu[q] * W + slot * VW);
+      }
+#pragma unroll
+      for (int q = 0; q < PB; ++q)
+#pragma unroll
+        for (int j = 0; j < VW; ++j) a.w[j] |= x[q].w[j];
+    }
+    // one cross-group OR and coverage check per tile
+#pragma unroll
+    for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < VW; ++j) a.w[j] |= __shfl_xor(a.w[j], off);
+    bool cov = true;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) cov &= (a.w[j] & unv.w[j]) == unv.w[j];
+    if (!__ballot(!cov)) covered = true;
+    __builtin_amdgcn_wave_barrier();  // lst is rewritten by the next tile
+  }
+  if (sub == 0) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const uint64_t nb = a.w[j] & unv.w[j];
+      if (nb) atomicOr((unsigned long long*)&acc[vo + j], nb);
+    }
+  }
+}
+
 // Chunk descriptor: vertex, first column position, edge count (<= kChunk). Built once per level
 // by k_chunk_desc; a wave reads its next descriptor with one scalar load while it pulls the
 // current chunk (vs an owner -> list entry -> row offsets chain of dependent loads per chunk).
@@ -1002,7 +1115,8 @@ static __global__ __launch_bounds__(kBlock) void k_chunk_rest_desc(const int32_t
   }
 }
 
-template <int W, int T, int BT, int HUBW>
+// PFXL: the chunks of a prefix-pull level without codes (chunk_pull_pfx)
+template <int W, int T, int BT, int HUBW, bool PFXL = false>
 __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_bu_chunks(
     const ChunkDesc* __restrict__ desc, const int64_t* nchunks_p, const int32_t* col,
     const uint64_t* R,
@@ -1041,8 +1155,11 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
     const int64_t beg = uni64((int64_t)(((uint64_t)d.beg_hi << 32) | d.beg_lo));
     const int64_t lim = beg + uni32(d.len);
     if (c + cstep < cend) d = desc[c + cstep];  // next descriptor, in flight during the pull
-    chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop,
-                           lst, code, code_from, wacc[threadIdx.x >> 6], snap, dsnap);
+    if constexpr (PFXL)
+      chunk_pull_pfx<W, T, HUBW>(v, beg, lim, col, R, am, acc, hub, lst, snap);
+    else
+      chunk_pull<W, T, HUBW>(v, beg, lim, col, R, am, acc, anyvis, hub, filter_from, coop,
+                             lst, code, code_from, wacc[threadIdx.x >> 6], snap, dsnap);
   }
 }
 

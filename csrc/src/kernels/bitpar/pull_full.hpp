@@ -188,7 +188,13 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   if (v1 < 0) e1 = b1;
   constexpr int F1 = C1 > 0 ? C1 : C;  // neighbours of the first step
   // column entries [b, b + F1) of a row [b, e): slot q*G + lane's entry, -1 past the end
+  // (one lane per vertex and four-entry steps: col4_aligned)
+  constexpr bool A4 = G == 1 && Q == 4;
   auto first_ids = [&](int64_t b, int64_t e, int32_t (&u)[Q]) {
+    if constexpr (A4 && F1 == 4) {
+      col4_aligned(col, b, e, u);
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int k = q * G + slot;
@@ -211,6 +217,10 @@ __global__ __launch_bounds__(kBlock, W <= 2 ? 5 : 4) void k_bu_full(
   };
   // column entries [e, e + C) of a row ending at `end`: slot q*G + lane's entry, -1 past the end
   auto step_ids = [&](int64_t e, int64_t end, int32_t (&u)[Q]) {
+    if constexpr (A4) {
+      col4_aligned(col, e < end ? e : 0, e < end ? end : 0, u);
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int64_t ee = e + q * G + slot;

@@ -384,7 +384,11 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       // with the 128-KB hub bitmap (ids < 1M) except on the prefix level, whose prefixes end
       // at the small one's bound (two blocks per CU)
       const bool big = hub_big && !pfx;
-      auto ck = big ? k_bu_chunks<W, 256, 1024, kHubBig> : k_bu_chunks<W, 256, 1024, kHubW>;
+      // (the prefix level without codes: LDS probes only, the next tile's ids in flight)
+      auto ck = big ? k_bu_chunks<W, 256, 1024, kHubBig>
+                    : (pfx && !codes && filter_from == 0 && !dprobe && !coop)
+                          ? k_bu_chunks<W, 256, 1024, kHubW, true>
+                          : k_bu_chunks<W, 256, 1024, kHubW>;
       ck<<<grid_for(maxc, 16, big ? 256 : 512), 1024, 0, s>>>(
           d, np, g_.col, R, alive, sm.gmask, acc_[S.ac].as<uint64_t>(), anyvis_.as<uint32_t>(),
           filter_from, coop, codes, code_from, snap, dprobe);

@@ -58,13 +58,29 @@ def init_from_env(backend: Optional[str] = None, gpus_per_node: Optional[int] = 
     """Initialise from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
 
     Device binding follows the reference: device = local_rank % gpus_per_node (main.cu:227).
-    """
-    import torch
-    import torch.distributed as dist
 
+    A single process (world 1, not forced) never imports torch: the native engine drives the GPU
+    alone, so the process holds one HIP runtime (the system's). torch's wheel bundles its own
+    ROCm libraries; next to them rocprofv3's runtime tracer crashed in its exit-time finalizer
+    (round 5: tools/exit_check.py, frames in librocprofiler-sdk -> libhsa-runtime64).
+    """
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    forced = world == 1 and os.environ.get("MSBFS_FORCE_DIST") == "1"
+    if world == 1 and not forced:
+        from ..ops import native
+        device = -1
+        if use_gpu is None or use_gpu:
+            ngpu = native.device_count()
+            if use_gpu and ngpu < 1:
+                raise RuntimeError("no GPU visible")
+            if ngpu >= 1:
+                device = 0
+        return DistContext(0, 1, 0, device, "none")
+    import torch
+    import torch.distributed as dist
+
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
     device = -1
@@ -75,7 +91,6 @@ def init_from_env(backend: Optional[str] = None, gpus_per_node: Optional[int] = 
         torch.cuda.set_device(device)
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
-    forced = world == 1 and os.environ.get("MSBFS_FORCE_DIST") == "1"
     if world > 1 or forced:
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -91,8 +106,10 @@ def init_from_env(backend: Optional[str] = None, gpus_per_node: Optional[int] = 
 
 
 def shutdown(ctx: DistContext) -> None:
+    if not ctx.distributed:
+        return
     import torch.distributed as dist
-    if ctx.distributed and dist.is_initialized():
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -136,8 +153,8 @@ def _reduce_small(a: np.ndarray, ctx: DistContext, op) -> np.ndarray:
 
 
 def barrier(ctx: DistContext) -> None:
-    import torch.distributed as dist
     if ctx.distributed:
+        import torch.distributed as dist
         if ctx.backend == "nccl":
             dist.barrier(device_ids=[ctx.device])
         else:
@@ -229,16 +246,16 @@ def _qbits(K: int) -> int:
 
 
 def allreduce_max(x: float, ctx: DistContext) -> float:
-    import torch.distributed as dist
     if not ctx.distributed:
         return float(x)
+    import torch.distributed as dist
     return float(_reduce_small(np.array([float(x)], np.float64), ctx, dist.ReduceOp.MAX)[0])
 
 
 def allreduce_sum_i64(a: np.ndarray, ctx: DistContext) -> np.ndarray:
-    import torch.distributed as dist
     if not ctx.distributed:
         return a
+    import torch.distributed as dist
     return _reduce_small(np.ascontiguousarray(a, dtype=np.int64), ctx, dist.ReduceOp.SUM)
 
 
@@ -250,8 +267,6 @@ def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistC
     62 bits with the query index sends key 0 instead, which every rank then sees as the MIN: all of
     them take the two-all-reduce fallback together.
     """
-    import torch.distributed as dist
-
     F_local = np.asarray(F_local, dtype=np.int64)
     idx_local = np.asarray(idx_local, dtype=np.int64)
     qb = _qbits(K)
@@ -260,6 +275,7 @@ def packed_argmin(F_local: np.ndarray, idx_local: np.ndarray, K: int, ctx: DistC
     def allmin(v: int) -> int:
         if not ctx.distributed:
             return v
+        import torch.distributed as dist
         return int(_reduce_small(np.array([v], np.int64), ctx, dist.ReduceOp.MIN)[0])
 
     maxF = int(F_local.max()) if len(F_local) else 0
@@ -299,9 +315,6 @@ class AsyncArgmin:
         self._stream = None
 
     def start(self, F_local: np.ndarray, idx_local: np.ndarray, K: int):
-        import torch
-        import torch.distributed as dist
-
         F_local = np.asarray(F_local, dtype=np.int64)
         idx_local = np.asarray(idx_local, dtype=np.int64)
         qb = _qbits(K)
@@ -313,6 +326,9 @@ class AsyncArgmin:
         pend = {"F": F_local, "idx": idx_local, "K": K, "qb": qb, "key": key}
         if not self.ctx.distributed:
             return pend
+        import torch
+        import torch.distributed as dist
+
         dev = _comm_device(self.ctx)
         if dev.type != "cuda":
             t = torch.tensor([key], dtype=torch.int64)

@@ -47,6 +47,10 @@ def main(mode: str) -> int:
                 s.close()
         if mode != "leak":
             g.close()
+    # the executable mappings, to name the frames of a teardown crash's stack afterwards
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("/proc/self/maps") as f, open(f"gpurun_out/maps_{mode}.txt", "w") as o:
+        o.writelines(l for l in f if " r-xp " in l)
     print(f"exit_check {mode} done", flush=True)
     return 0
 
