@@ -46,6 +46,51 @@ __device__ __forceinline__ void col4_aligned(const int32_t* col, int64_t b, int6
   }
 }
 
+// lanes below this one among the set bits of a wave mask (v_mbcnt)
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Wave-private LDS queue: items of this wave only; the count is wave-uniform (kept in an SGPR),
+// a flush takes one global atomic for the whole run and writes it out coalesced.
+__device__ __forceinline__ void wq_push(int32_t* q, uint32_t& n, bool pred, int32_t v) {
+  const uint64_t m = __ballot(pred);
+  if (pred) q[n + mbcnt64(m)] = v;
+  n += (uint32_t)__popcll(m);
+}
+__device__ __forceinline__ void wq_flush(int32_t* q, uint32_t& n, int32_t* out, uint32_t* gcnt) {
+  if (!n) return;
+  uint32_t base = 0;
+  if (lane_id() == 0) base = atomicAdd(gcnt, n);
+  base = __builtin_amdgcn_readfirstlane(base);
+  for (uint32_t i = lane_id(); i < n; i += 64) out[base + i] = q[i];
+  n = 0;
+}
+
+// The end-of-kernel flush of every wave's queue: the block's waves publish their counts, one
+// lane takes the block's run with one atomic, each wave writes its items at its offset.
+// Block-uniform (every thread calls it); wbase: kWaves + 1 LDS words.
+__device__ __forceinline__ void wq_flush_block(int32_t* q, uint32_t& n, int32_t* out,
+                                               uint32_t* gcnt, uint32_t* wbase) {
+  const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  __syncthreads();
+  if (lane_id() == 0) wbase[wv] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < nwv; ++w) {
+      const uint32_t c = wbase[w];
+      wbase[w] = t;
+      t += c;
+    }
+    wbase[nwv] = t ? atomicAdd(gcnt, t) : 0u;
+  }
+  __syncthreads();
+  const uint32_t base = wbase[nwv] + wbase[wv];
+  for (uint32_t i = lane_id(); i < n; i += 64) out[base + i] = q[i];
+  n = 0;
+}
+
 template <int VW>
 struct V {
   uint64_t w[VW];

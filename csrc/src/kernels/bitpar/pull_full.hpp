@@ -33,11 +33,6 @@ __device__ __forceinline__ void st_row(uint64_t* base, int32_t u, int voff, cons
   stv<VW>(base + (int64_t)u * W + voff / 8, r);
 }
 
-// lanes below this one among the set bits of a wave mask (v_mbcnt)
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
 // Value of lane (group base + K) for every lane of a group of G lanes (G <= 8 never crosses the
 // 32-lane halves ds_swizzle's bitmask mode works in): and-mask keeps the group bits, or-mask
 // selects the lane.
@@ -57,22 +52,6 @@ __device__ __forceinline__ void bcast_ids(const int32_t (&u)[Q], int32_t (&uc)[N
   ((uc[Ks] = group_bcast<G, Ks % G>(u[Ks / G])), ...);
 }
 
-// Wave-private LDS queue: items of this wave only; the count is wave-uniform (kept in an SGPR),
-// a flush takes one global atomic for the whole run and writes it out coalesced.
-__device__ __forceinline__ void wq_push(int32_t* q, uint32_t& n, bool pred, int32_t v) {
-  const uint64_t m = __ballot(pred);
-  if (pred) q[n + mbcnt64(m)] = v;
-  n += (uint32_t)__popcll(m);
-}
-__device__ __forceinline__ void wq_flush(int32_t* q, uint32_t& n, int32_t* out, uint32_t* gcnt) {
-  if (!n) return;
-  uint32_t base = 0;
-  if (lane_id() == 0) base = atomicAdd(gcnt, n);
-  base = __builtin_amdgcn_readfirstlane(base);
-  for (uint32_t i = lane_id(); i < n; i += 64) out[base + i] = q[i];
-  n = 0;
-}
-
 // Done rows are never read (tuning key dskip, BitparSolver::level_bu): a vertex that is done (every
 // alive group visited) has every group alive now, so a pull may OR the alive mask instead of its
 // row. dsnap = the done bitmap as of the level start (a vertex done during this level may hold
@@ -82,30 +61,6 @@ __device__ __forceinline__ void wq_flush(int32_t* q, uint32_t& n, int32_t* out, 
 // one reader that needs such a row, a push level right after, gets it from k_fix_done_rows.
 __device__ __forceinline__ bool done_in(const uint32_t* snap, int32_t u) {
   return u >= 0 && ((snap[u >> 5] >> (u & 31)) & 1u);
-}
-
-// The end-of-kernel flush of every wave's queue: the block's waves publish their counts, one
-// lane takes the block's run with one atomic, each wave writes its items at its offset.
-// Block-uniform (every thread calls it); wbase: kWaves + 1 LDS words.
-__device__ __forceinline__ void wq_flush_block(int32_t* q, uint32_t& n, int32_t* out,
-                                               uint32_t* gcnt, uint32_t* wbase) {
-  const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  __syncthreads();
-  if (lane_id() == 0) wbase[wv] = n;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < nwv; ++w) {
-      const uint32_t c = wbase[w];
-      wbase[w] = t;
-      t += c;
-    }
-    wbase[nwv] = t ? atomicAdd(gcnt, t) : 0u;
-  }
-  __syncthreads();
-  const uint32_t base = wbase[nwv] + wbase[wv];
-  for (uint32_t i = lane_id(); i < n; i += 64) out[base + i] = q[i];
-  n = 0;
 }
 
 // CS neighbours per step; C1 > 0: a first step of only C1 rows (late levels are mostly covered by
