@@ -41,22 +41,48 @@ __device__ __forceinline__ void q_push(LdsQueueN<CAP>& q, bool pred, int32_t v) 
   if (pred) q.item[pos] = v;
 }
 
-// Flush the queue to out[] when it may not hold another `room` items (or always, at the end).
-// Must be called by every thread of the block (block-uniform control flow).
+// Flush each of NQ queues to its out[] when it may not hold another `room` items (or always, at
+// the end), sharing the barriers: two when nothing is flushed, four otherwise (the pull kernels
+// check three queues after every tile; flushed one at a time they paid up to 15 barriers a tile).
+// Must be called by every thread of the block (block-uniform control flow); blockDim >= NQ.
+template <int CAP, int NQ>
+__device__ __forceinline__ void q_flush_n(LdsQueueN<CAP>* const (&q)[NQ], int32_t* const (&out)[NQ],
+                                          uint32_t* const (&gcnt)[NQ], int room, bool force) {
+  __syncthreads();
+  uint32_t n[NQ];
+  bool f[NQ], any = false;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    n[i] = q[i]->n;
+    f[i] = n[i] != 0 && (force || n[i] + (uint32_t)room > (uint32_t)CAP);
+    any |= f[i];
+  }
+  __syncthreads();  // every count read before any push or reset
+  if (!any) return;
+  // (no pushes until the last barrier: the counts may be reset here)
+#pragma unroll
+  for (int i = 0; i < NQ; ++i)
+    if (f[i] && threadIdx.x == (unsigned)i) {
+      q[i]->base = atomicAdd(gcnt[i], n[i]);
+      q[i]->n = 0;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    if (!f[i]) continue;
+    const uint32_t base = q[i]->base;
+    for (uint32_t j = threadIdx.x; j < n[i]; j += blockDim.x) out[i][base + j] = q[i]->item[j];
+  }
+  __syncthreads();  // items read before the next pushes overwrite them
+}
+
 template <int CAP>
 __device__ __forceinline__ void q_flush(LdsQueueN<CAP>& q, int32_t* out, uint32_t* gcnt, int room,
                                         bool force) {
-  __syncthreads();
-  const uint32_t n = q.n;
-  __syncthreads();
-  if (n == 0 || (!force && n + (uint32_t)room <= (uint32_t)CAP)) return;
-  if (threadIdx.x == 0) q.base = atomicAdd(gcnt, n);
-  __syncthreads();
-  const uint32_t base = q.base;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[base + i] = q.item[i];
-  __syncthreads();
-  if (threadIdx.x == 0) q.n = 0;
-  __syncthreads();
+  LdsQueueN<CAP>* const qs[1] = {&q};
+  int32_t* const os[1] = {out};
+  uint32_t* const cs[1] = {gcnt};
+  q_flush_n<CAP, 1>(qs, os, cs, room, force);
 }
 
 // block-wide sum of per-thread values, one atomic per block; scratch holds blockDim/64 values

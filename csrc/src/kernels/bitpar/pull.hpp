@@ -314,8 +314,10 @@ __global__ __launch_bounds__(kBlock) void k_push_tail_after(
 // CS = neighbours per step (rows gathered between two coverage checks).
 // C1 > 0 (unfiltered levels only): a first step of just C1 rows before the CS-wide steps; late
 // levels are mostly covered by the first neighbour or two (sorted rows: hubs first).
+// FBM: the new frontier goes into the bitmap fbm (passed as fl2) and its size into ctr->fl2, no
+// frontier list (the prefix level at few words, whose next level pulls: see level_bu).
 template <int W, bool COUNT, int BT, int HUBW, bool FUSE, bool FILT = true, bool PFX = false,
-          int CS = 8, int C1 = 0, int MINW = 4>
+          int CS = 8, int C1 = 0, int MINW = 4, bool FBM = false>
 __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
     const int32_t* act, int64_t nact, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, uint64_t* Wb, const uint64_t* alive, const uint64_t* gmask, uint32_t* done,
@@ -360,6 +362,8 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
 #pragma unroll
   for (int j = 0; j < VW; ++j) am.w[j] = alive[slot * VW + j] & gmask[slot * VW + j];
   unsigned long long eu = 0, ef = 0, ev = 0;
+  uint32_t nfc = 0;  // FBM: new frontier vertices
+  __shared__ uint32_t scratch32[FBM ? NWV : 1];
   BitCounter<VW, PFX ? 5 : 6> bc;
   int nadd = 0;
   if constexpr (FUSE) bc.zero();
@@ -552,14 +556,23 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
     first_ids(idx + stride < nact, u1);
     q_push(qa, keep && (int)deg <= next_wide, v);
     q_push(qw, keep && (int)deg > next_wide, v);
-    q_push(qf, app, v);
-    q_flush(qa, act2, &ctr->act2.v, TILE, false);
-    q_flush(qw, actw2, &ctr->actw2.v, TILE, false);
-    q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
+    if constexpr (FBM) {
+      wave_set_bits<true>(reinterpret_cast<uint32_t*>(fl2), v, app);
+      nfc += app ? 1u : 0u;
+      q_flush_n<kQCap, 2>({&qa, &qw}, {act2, actw2}, {&ctr->act2.v, &ctr->actw2.v}, TILE, false);
+    } else {
+      q_push(qf, app, v);
+      q_flush_n<kQCap, 3>({&qa, &qw, &qf}, {act2, actw2, fl2},
+                          {&ctr->act2.v, &ctr->actw2.v, &ctr->fl2.v}, TILE, false);
+    }
   }
-  q_flush(qa, act2, &ctr->act2.v, 0, true);
-  q_flush(qw, actw2, &ctr->actw2.v, 0, true);
-  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  if constexpr (FBM) {
+    q_flush_n<kQCap, 2>({&qa, &qw}, {act2, actw2}, {&ctr->act2.v, &ctr->actw2.v}, 0, true);
+    block_sum_add32(nfc, &ctr->fl2.v, scratch32);
+  } else {
+    q_flush_n<kQCap, 3>({&qa, &qw, &qf}, {act2, actw2, fl2},
+                        {&ctr->act2.v, &ctr->actw2.v, &ctr->fl2.v}, 0, true);
+  }
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);
   block_sum_add(ev, &ctr->ev2.v, scratch);
@@ -1164,7 +1177,7 @@ __global__ __launch_bounds__(BT, (BT >= 1024 && HUBW <= 16384) ? 8 : 4) void k_b
 }
 
 // bottom-up, wide vertices, phase 2: G lanes per vertex fold acc[v] into the visited words.
-template <int W, bool COUNT, bool FUSE>
+template <int W, bool COUNT, bool FUSE, bool FLB = false>
 __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const int32_t* wl, int64_t nw, const int64_t* rowptr, const uint64_t* R, uint64_t* Wb,
     uint64_t* acc, const uint64_t* alive, const uint64_t* gmask, uint32_t* done, int32_t* actw2,
@@ -1172,7 +1185,9 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const uint32_t* snap, uint32_t* fbm = nullptr) {
   // fbm != nullptr (the tiled first pull level, see tiles.hpp): wl is the static big-vertex list,
   // so done vertices are skipped; no list queues: the new frontier goes into bitmap fbm and its
-  // size into ctr->fl2, the next active lists come from k_build_active after the level
+  // size into ctr->fl2, the next active lists come from k_build_active after the level.
+  // FLB (with fbm, the narrow pull's FBM levels): wl is the level's wide active list; only the
+  // frontier goes into fbm, the next active lists are built here as without fbm.
   using L = Lay<W>;
   constexpr int VW = L::VW, G = L::G, VPW = L::VPW, TILE = L::TILE;
   // done / any-visited bits: one atomic per word of the wave (wave_set_bits) where a wave
@@ -1210,7 +1225,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     uint32_t deg = 0;
     if (valid) {
       v = wl[idx];
-      if (fbm && is_done(done, v)) {
+      if (fbm && !FLB && is_done(done, v)) {
         // (the tiled level's tail push also pushes into done vertices: leave their acc row clean;
         // and give them their unchanged row in Wb, which k_push_tail_after filters against)
         const int64_t vo = (int64_t)v * W + slot * VW;
@@ -1250,7 +1265,7 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     const bool leader = valid && slot == 0;
     wave_set_bits<kCombine>(done, v, leader && !g_nf);
     const bool keep = leader && g_nf, app = leader && g_new;
-    if (keep && !fbm) eu += deg;
+    if (keep && (!fbm || FLB)) eu += deg;
     if (app) ef += deg;
     {
       const bool g_first = g_new && !((__ballot(rnz) >> (sub * G)) & L::GBITS);
@@ -1260,18 +1275,17 @@ __global__ __launch_bounds__(kBlock) void k_bu_wide_finalize(
     if (fbm) {  // (uniform)
       wave_set_bits<kCombine>(fbm, v, app);
       nfc += app ? 1u : 0u;
-      continue;
+      if (!FLB) continue;
+    } else {
+      q_push(qf, app, v);
     }
     q_push(qa, keep && (int)deg > next_wide, v);
     q_push(qn, keep && (int)deg <= next_wide, v);
-    q_push(qf, app, v);
-    q_flush(qa, actw2, &ctr->actw2.v, TILE, false);
-    q_flush(qn, act2n, &ctr->act2.v, TILE, false);
-    q_flush(qf, fl2, &ctr->fl2.v, TILE, false);
+    q_flush_n<kQCap, 3>({&qa, &qn, &qf}, {actw2, act2n, fl2},
+                        {&ctr->actw2.v, &ctr->act2.v, &ctr->fl2.v}, TILE, false);
   }
-  q_flush(qa, actw2, &ctr->actw2.v, 0, true);
-  q_flush(qn, act2n, &ctr->act2.v, 0, true);
-  q_flush(qf, fl2, &ctr->fl2.v, 0, true);
+  q_flush_n<kQCap, 3>({&qa, &qn, &qf}, {actw2, act2n, fl2},
+                      {&ctr->actw2.v, &ctr->act2.v, &ctr->fl2.v}, 0, true);
   if (fbm) block_sum_add32(nfc, &ctr->fl2.v, scratch32);
   block_sum_add(eu, &ctr->eu2.v, scratch);
   block_sum_add(ef, &ctr->ef2.v, scratch);

@@ -260,6 +260,14 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     }
   }
   const int32_t* plen = pfx ? prefix_lens(kPfxH, s) : nullptr;
+  // the untiled prefix level (few words) writes its frontier as a bitmap (fbm_tile_, as the tiled
+  // one): the next level pulls and reads no list, a push materialises it (materialize_frontier)
+  const bool fbm_out = pfx && FUSE && !tiled && S.nact + S.nactw > 0;
+  if (fbm_out) {
+    const int64_t nwords = (g_.n + 31) / 32;
+    fbm_tile_.ensure((size_t)(nwords + 1) * sizeof(uint32_t));
+    MSBFS_HIP_CHECK(hipMemsetAsync(fbm_tile_.p, 0, (size_t)nwords * sizeof(uint32_t), s));
+  }
   // (see k_push_tail_after; needs the whole level in one tiles launch and vertex part 0 of 1)
   S.push_after = pfx && tiled && tun_.push_after && S.nparts == 1 && !S.on_chunk;
   if (pfx && !S.push_after) {
@@ -285,15 +293,22 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     S.have_active = S.level < S.stop_level;
   } else if (S.nact) {
     if (pfx) {
-      constexpr int BT = 1024;
+      // one word: 80 VGPRs, 6 waves per SIMD, so two 768-thread blocks per CU (the 56-KB hub
+      // bitmap each) instead of one 1024-thread block: RMAT-30 / 32 groups level 2 35.9 -> 32.8
+      // ms, RMAT-26 / 16 groups 3.53 -> 3.36 ms (a next-step column id prefetch measured slower:
+      // 88 VGPRs)
+      constexpr int BT = W == 1 ? 768 : 1024;
       const int gn = grid_for(S.nact, (BT / 64) * L::VPW, 512);
       // 4-neighbour steps: 122 VGPRs, no spills (8-neighbour steps spilled at the 128-VGPR
       // bound): RMAT-26 5.17 -> 4.96 ms (the full pulls of level 3 keep 8: 5.8 vs 6.8 ms)
-      auto kn = FUSE ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE, true, true, 4>
+      // (FBM: frontier bitmap in place of the list, see fbm_out)
+      auto kn = FUSE ? k_bu_narrow<W, COUNT, BT, kHubW, FUSE, true, true, 4, 0, (W == 1 && BT < 1024 ? 6 : 4), true>
                      : k_bu_narrow<W, COUNT, BT, kHubW, false, true, true>;
       kn<<<gn, BT, 0, s>>>(act_[0].as<int32_t>(), S.nact, g_.rowptr, g_.col, R, O, alive,
                            sm.gmask, done_.as<uint32_t>(), act_[1].as<int32_t>(),
-                           fl_[S.fc ^ 1].as<int32_t>(), ctr_.as<Ctr>(),
+                           FUSE ? reinterpret_cast<int32_t*>(fbm_tile_.p)
+                                : fl_[S.fc ^ 1].as<int32_t>(),
+                           ctr_.as<Ctr>(),
                            anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
                            next_wide, slabF<W>(rows), acc_[S.ac].as<uint64_t>(),
                            stamp_.as<int32_t>(), epoch_, plen, nullptr, snap, BuGate{});
@@ -444,11 +459,13 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   }
   if (S.nactw && !tiled) {
     const int gw = grid_for(S.nactw, L::TILE, grid);
-    k_bu_wide_finalize<W, COUNT, FUSE><<<gw, kBlock, 0, s>>>(
+    auto kw = fbm_out ? k_bu_wide_finalize<W, COUNT, FUSE, true>
+                      : k_bu_wide_finalize<W, COUNT, FUSE>;
+    kw<<<gw, kBlock, 0, s>>>(
         actw_[0].as<int32_t>(), S.nactw, g_.rowptr, R, O, acc_[S.ac].as<uint64_t>(), alive,
         sm.gmask, done_.as<uint32_t>(), actw_[1].as<int32_t>(), fl_[S.fc ^ 1].as<int32_t>(),
         ctr_.as<Ctr>(), anyvis_.as<uint32_t>(), act_[1].as<int32_t>(), next_wide,
-        slabF<W>(rows), snap);
+        slabF<W>(rows), snap, fbm_out ? fbm_tile_.as<uint32_t>() : nullptr);
     MSBFS_HIP_CHECK(hipGetLastError());
     if (FUSE) rows += gw;
   }
@@ -466,6 +483,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   S.cur ^= 1;
   S.fsrc_acc = false;
   S.osnap_next = lazy_first;
+  if (fbm_out) S.fl_bitmap = true;
   return rows;
 }
 

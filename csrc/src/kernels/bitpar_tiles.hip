@@ -263,12 +263,13 @@ int BitparSolver::tiles_pull(Loop& S, hipStream_t s, const uint64_t* R, uint64_t
   return rows;
 }
 
-// fl_[fc] from the frontier bitmap of a tiled level (only a top-down level reads the list)
+// fl_[fc] from the frontier bitmap of a prefix level (only a top-down level reads the list)
 void BitparSolver::materialize_frontier(Loop& S, hipStream_t s) {
   if (!S.fl_bitmap) return;
   S.fl_bitmap = false;
   if (S.nf <= 0) return;
   const int64_t nwords = (g_.n + 31) / 32;
+  lcnt_.ensure(sizeof(Ctr));  // (also left by the untiled prefix level, see level_bu)
   MSBFS_HIP_CHECK(hipMemsetAsync(lcnt_.p, 0, sizeof(Ctr), s));
   k_bitmap_list<<<grid_for(nwords, kBlock, 2048), kBlock, 0, s>>>(
       fbm_tile_.as<uint32_t>(), nwords, fl_[S.fc].as<int32_t>(), lcnt_.as<Ctr>());
