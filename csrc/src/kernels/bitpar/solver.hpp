@@ -102,6 +102,10 @@ struct Tuning {
   // RMAT-26, level 2, 128 groups 6.54 -> 6.01 ms, 256 groups 7.49 -> 7.11 ms (32 -> 128; 512 and
   // 2048 slower; RMAT-22 prefers 32-64). 0: wide_degree as given
   int wide_few = 128;
+  // prefix bound of the untiled first pull level (ids below it are pulled, the frontier vertices
+  // at or above it push; <= 458752, the LDS hub bitmap's bound). 0: from the batch's source
+  // count (BitparSolver::pfx_bound)
+  int pfx_h = 0;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->
@@ -148,6 +152,7 @@ class BitparSolver final : public Solver {
     int alv = 0;  // alive[alv] = groups with a non-empty frontier
     uint32_t level = 0;
     int64_t nf = 0, ef = 0, ev = 0, na = 0, ea = 0, nact = 0, nactw = 0;
+    int64_t nsrc = 0;  // the batch's (source, group) pairs
     bool have_active = false, fsrc_acc = true, bottom_up = false;
     int bu_levels = 0;
     // limits
@@ -228,6 +233,8 @@ class BitparSolver final : public Solver {
   template <int W, bool COUNT>
   void bu_batch(Loop& S, RunStats* st, hipStream_t s);
   const int32_t* prefix_lens(int32_t H, hipStream_t s);
+  template <int W>
+  int32_t pfx_bound(const Loop& S);  // prefix bound of the untiled prefix level
   // ---- bitpar_tiles.hip: the first pull level's prefix pull over static vertex tiles
   struct TileSet {
     DevBuf pent, tiles, big;

@@ -71,6 +71,27 @@ int32_t BitparSolver::code_bound(double min_deg) {
   return deg_bounds_[k];
 }
 
+// Prefix bound H of the untiled prefix level. Pulling the ids of [a, b) costs a column entry per
+// edge into the range (every active vertex scans its prefix); pushing them costs a scattered
+// atomic per edge of the range's frontier vertices only. A random source is adjacent to u with
+// probability ~deg(u)/n, so with S sources u is a level-1 frontier vertex with probability
+// ~S deg(u)/n: the pull pays where that is >= 1/(64 W) (a push is W atomics per edge). Measured
+// with tuning pfx_h: RMAT-30 / 32 groups best at H = 32768 (level 2 33.0 -> 28.7 ms), RMAT-26 /
+// 16 groups at 32768-131072 (3.38 -> 3.02 ms), RMAT-22 / 64 groups near 131072, RMAT-26 / 128
+// groups (2 words) at the hub bitmap's bound.
+template <int W>
+int32_t BitparSolver::pfx_bound(const Loop& S) {
+  constexpr int32_t kPfxH = 14336 * 32;  // (the LDS hub bitmap's bound, see level_bu)
+  if (tun_.pfx_h > 0) return std::min(tun_.pfx_h, kPfxH);
+  if (S.nsrc <= 0) return kPfxH;
+  const double md = (double)g_.n / (64.0 * W * (double)S.nsrc);  // degree where the pull pays
+  if (md < 2.0) return kPfxH;
+  int k = 0;
+  while (k + 1 < kDegBounds && (double)((int64_t)1 << (k + 1)) <= md) ++k;  // 2^k <= md
+  const int32_t h = code_bound((double)((int64_t)1 << k));  // vertices of degree >= 2^k
+  return h <= 0 ? kPfxH : std::min(std::max(h, 1024), kPfxH);
+}
+
 // Everything a run would otherwise build or allocate on first use, so that no timed run pays
 // for it (the CLI's computation phase, main.cu:301-400): the vertex extent, the prefix
 // lengths and first-neighbour array, the degree-bound table, and the worst-case chunk
@@ -259,7 +280,11 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
       code_from = kNoCodes;
     }
   }
-  const int32_t* plen = pfx ? prefix_lens(kPfxH, s) : nullptr;
+  // prefix bound: the tiles' fixed one, or pfx_bound for the per-vertex prefix pull (plen is
+  // cached for one bound: a batch with another source count rebuilds it, one pass over the rows)
+  // (the tiles hold their entries: no prefix lengths read at run time)
+  const int32_t H = tiled ? kPfxH : pfx_bound<W>(S);
+  const int32_t* plen = pfx && !tiled ? prefix_lens(H, s) : nullptr;
   // the untiled prefix level (few words) writes its frontier as a bitmap (fbm_tile_, as the tiled
   // one): the next level pulls and reads no list, a push materialises it (materialize_frontier)
   const bool fbm_out = pfx && FUSE && !tiled && S.nact + S.nactw > 0;
@@ -273,7 +298,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   if (pfx && !S.push_after) {
     ++epoch_;
     k_push_tail<W><<<grid_for(S.nf * 64, kBlock, 8192), kBlock, 0, s>>>(
-        fl_[S.fc].as<int32_t>(), S.nf, kPfxH, g_.rowptr, g_.col, R, codes, code_from,
+        fl_[S.fc].as<int32_t>(), S.nf, H, g_.rowptr, g_.col, R, codes, code_from,
         tiled ? nullptr : done_.as<uint32_t>(), S.part, S.nparts, acc_[S.ac].as<uint64_t>(),
         tiled ? nullptr : stamp_.as<int32_t>(), epoch_);
     MSBFS_HIP_CHECK(hipGetLastError());

@@ -51,6 +51,10 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "dskip3") dskip3 = (int)to_num(key, v);
   else if (key == "chunk2") chunk2 = (int)to_num(key, v);
   else if (key == "wide_few") wide_few = (int)to_num(key, v);
+  else if (key == "pfx_h") {
+    pfx_h = (int)to_num(key, v);
+    if (pfx_h < 0 || pfx_h > 458752) fail("tuning: pfx_h must be in [0, 458752]");
+  }
   else if (key == "tiles_w") {
     tiles_w = (int)to_num(key, v);
     if (tiles_w != 4 && tiles_w != 8 && tiles_w != 16) fail("tuning: tiles_w must be 4, 8 or 16");
@@ -61,7 +65,7 @@ void Tuning::set(const std::string& key, const std::string& v) {
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip push_after dskip3 chunk2 wide_few tiles_w dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip push_after dskip3 chunk2 wide_few pfx_h tiles_w dirs)");
   }
 }
 
@@ -202,6 +206,7 @@ void BitparSolver::start_batch(int64_t k0, int64_t nb, const int64_t* qoff, cons
       }
     }
   const int64_t np = (int64_t)hp.size();
+  S.nsrc = np;
   // the batch's masks and source pairs go up from one pinned staging buffer (pageable copies
   // stage through the runtime and now and then stalled a step: RMAT-26 / 1024 groups, 1 step in
   // ~10-30 took +6 ms outside the level loop, tools/step_split.py); the read_ctr below retires

@@ -284,6 +284,36 @@ def test_bitpar_prefix_pull_tail_push(msbfs_pkg):
     g.close()
 
 
+@pytest.mark.parametrize("K", [16, 40, 128])
+def test_bitpar_prefix_bound(msbfs_pkg, K):
+    """The untiled prefix level (1-2 words) with its bound H chosen from the source count
+    (BitparSolver::pfx_bound) or forced (tuning pfx_h): the per-vertex scans stop at the first id
+    >= H, the hub chunks end there, the frontier vertices >= H push, and the frontier is left as
+    a bitmap (materialised when a top-down level follows). Identical F for every bound, with a
+    top-down level right after, and equal to the per-group distance solver on a sample."""
+    m = msbfs_pkg
+    g = m.DeviceGraph.rmat(23, 16, 5, device=0)
+    g.relabel_by_degree()
+    qs = m.QuerySet.random(g.n, K, 16, seed=K + 3)
+    runs = {"auto": {}, "full": {"pfx_h": 458752}, "h1024": {"pfx_h": 1024},
+            "h32768": {"pfx_h": 32768}, "h5000": {"pfx_h": 5000}, "off": {"pfx": 0},
+            "td3": {"dirs": "TBT"}, "td3h1024": {"dirs": "TBT", "pfx_h": 1024}}
+    out = {}
+    for name, tun in runs.items():
+        with m.Solver(g, "bitpar", max_groups=qs.K, tuning=tun) as s:
+            s.prepare()
+            out[name] = s.run(qs).F
+            out[name + "2"] = s.run(qs).F
+            tr = s.level_trace()
+        assert "".join(t["dir"] for t in tr).startswith("TBT" if "td3" in name else "TB"), name
+    for name in out:
+        assert np.array_equal(out[name], out["off"]), name
+    sub = qs.subset(np.arange(0, K, 7))
+    with m.Solver(g, "dist") as ds:
+        assert np.array_equal(ds.run(sub).F, out["auto"][::7])
+    g.close()
+
+
 @pytest.mark.parametrize("K", [1024, 900, 512, 200])
 def test_bitpar_tiled_first_pull(msbfs_pkg, K):
     """The first pull level over static vertex tiles (k_pfx_tiles + big-vertex partial tiles +
