@@ -922,18 +922,24 @@ __device__ __forceinline__ void chunk_pull_pfx(int32_t v, int64_t beg, int64_t l
     lane_open |= unv.w[j] != 0;
   }
   if (!__ballot(lane_open)) return;  // wave-uniform
+  // ids of the tile at t0 (16-byte aligned): lane l takes entries t0 + 4l .. t0 + 4l + 3 with
+  // one aligned 16-byte load (a quarter of the address work of four 4-byte loads; a window past
+  // the chunk reads the chunk's first one instead, and an aligned window holding a valid entry
+  // never leaves its page), entries outside [beg, lim) are -1
+  static_assert(Q == 4, "one 16-byte window per lane");
+  typedef int32_t i4 __attribute__((ext_vector_type(4)));
+  const int64_t a0 = beg & ~(int64_t)3;
   auto load_ids = [&](int64_t t0, int32_t (&u)[Q]) {
+    const int64_t e = t0 + 4 * lane;
+    const i4 w = *(const i4*)(col + (e < lim ? e : a0));
+    const int32_t x[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int64_t e = t0 + q * 64 + lane;
-      const int32_t x = col[e < lim ? e : beg];
-      u[q] = e < lim ? x : -1;
-    }
+    for (int q = 0; q < Q; ++q) u[q] = (e + q >= beg && e + q < lim) ? x[q] : -1;
   };
   int32_t un[Q];
-  load_ids(beg, un);
+  load_ids(a0, un);
   bool covered = false;
-  for (int64_t t0 = beg; t0 < lim && !covered; t0 += T) {
+  for (int64_t t0 = a0; t0 < lim && !covered; t0 += T) {
     int32_t u[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) u[q] = un[q];
