@@ -291,7 +291,6 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
     bool nz = false, full = true;
     if (v < n_eff) {
       stv<VW>(visA + v * W + slot * VW, x);
-      stv<VW>(visB + v * W + slot * VW, x);
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
         nz |= x.w[j] != 0;
@@ -300,6 +299,9 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
     }
     const bool g_nz = (__ballot(nz) >> (sub * G)) & L::GBITS;
     const bool g_full = !((__ballot(!full) >> (sub * G)) & L::GBITS);
+    // the level-3 output buffer needs the rows of the vertices done now only: every active one
+    // gets its row from the level-3 pull (or is skipped there, dskip3, and never read again)
+    if (v < n_eff && g_full) stv<VW>(visB + v * W + slot * VW, x);
     if (slot == 0) {
       fullf[wv * VPW + sub] = v < n_eff && g_full;
       nzf[wv * VPW + sub] = g_nz;
@@ -308,8 +310,7 @@ __global__ __launch_bounds__(kBlock) void k_hybrid_setup(const uint64_t* recv, i
     if (actv) eu += (unsigned long long)deg;
     q_push(qn, actv && deg <= wide_deg, (int32_t)v);
     q_push(qw, actv && deg > wide_deg, (int32_t)v);
-    q_flush(qn, act, &ctr->act2.v, TILE, false);
-    q_flush(qw, actw, &ctr->actw2.v, TILE, false);
+    q_flush_n<2048, 2>({&qn, &qw}, {act, actw}, {&ctr->act2.v, &ctr->actw2.v}, TILE, false);
     for (int i = threadIdx.x; i < TILE / 32; i += kBlock) {
       const int64_t w32 = (tb >> 5) + i;
       if (w32 < nwords32) {
