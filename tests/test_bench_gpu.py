@@ -1,7 +1,9 @@
 """bench.py's multi-GPU code paths on the one-GPU box: MSBFS_FORCE_DIST=1 makes a one-rank
 torch.distributed process group over RCCL ("nccl") that still runs every collective (barrier,
-all-reduces, the hybrid all_to_all_single), and bench.py checks each decomposition's F vector
-against the round-robin pass before timing (exit status 3 on a mismatch)."""
+all-reduces, the hybrid exchange's point-to-point pieces), and bench.py checks each
+decomposition's F vector against the round-robin pass before timing (exit status 3 on a
+mismatch). Several ranks share the one GPU over gloo; the RCCL run with one GPU per rank needs a
+box with two or more GPUs and is skipped otherwise."""
 import json
 import os
 import socket
@@ -103,6 +105,29 @@ def test_bench_multi_rank_gloo_shared_gpu(ranks, dist):
         assert ph["chunks"] == (1 if dist == "hybrid-coded" else 8)
     else:
         assert set(cfg["candidates_ms"]) == {"roundrobin", "hybrid", "hybrid-coded"}
+
+
+def _visible_gpus():
+    import torch
+    return torch.cuda.device_count()  # (counts devices without creating a context)
+
+
+@pytest.mark.parametrize("dist", ["hybrid", "auto"])
+def test_bench_two_ranks_rccl(dist):
+    """Two ranks, one GPU each, over RCCL: the overlapped hybrid exchange's grouped P2P pieces
+    between real peers, the async argmin, and the candidates' F checked against round robin."""
+    if _visible_gpus() < 2:
+        pytest.skip("needs two GPUs (one per RCCL rank)")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--scale",
+                        "18", "--groups", "300", "--steps", "2", "--warmup", "1", "--dist", dist,
+                        "--verify", "4"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    cfg = js["config"]
+    assert js["n_gpus"] == 2 and cfg["devices"] == [0, 1] and cfg["candidate_errors"] == {}
+    if dist == "hybrid":
+        assert cfg["phases"]["chunks"] == 8
 
 
 @pytest.mark.parametrize("bad", ["hybrid", "hybrid-coded"])

@@ -208,7 +208,7 @@ def test_cli_gpu_many_passes_drain(tmp_path, msbfs_pkg, ranks, comm):
 def test_cli_gpu_hybrid_chunked_exchange(tmp_path, msbfs_pkg, ranks, comm, chunks):
     """--chunks N: the overlapped hybrid exchange (phase A hands out its vertex ranges, one
     all-to-all piece each; RCCL: grouped send/recv on the communicator's stream while phase A
-    goes on; host MPI: staged pieces). chunks 0 = the default (4 with RCCL)."""
+    goes on; host MPI: staged pieces). chunks 0 = the default (8 with RCCL)."""
     m = msbfs_pkg
     g, qs, gp, qp = _files(tmp_path, m, 300, 4)
     ref = m.cpu_bfs(g, qs, count_edges=True)

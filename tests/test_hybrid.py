@@ -403,6 +403,17 @@ def test_hybrid_tiled_phase_a(msbfs_pkg):
             b = s.hybrid_chunk_bounds(0, world, dg.hybrid_extent(), chunks)
             assert b[0] == 0 and b[-1] == H.part_count(dg.hybrid_extent(), 0, world)
             assert np.all(np.diff(b) >= 0) and len(b) == chunks + 1
+    # tiles from 4 words (tuning tiles_w = 4, 256 groups): the exchange ranges must start at
+    # tile starts for that word count too (a range split inside a tile would send rows that the
+    # next launch still changes), chunked and not
+    qs4 = qs.subset(np.arange(256))
+    with m.Solver(dg, "bitpar", max_groups=256, tuning={"tiles": 0}) as s:
+        ref4 = s.run(qs4).F
+    with m.Solver(dg, "bitpar", max_groups=256, tuning={"tiles_w": 4}) as s:
+        s.prepare()
+        for world, chunks in ((8, 4), (3, 5), (2, 1)):
+            assert np.array_equal(H.emulate_ranks(s, qs4, world, chunks=chunks), ref4), (world,
+                                                                                     chunks)
     dg.close()
 
 
