@@ -106,6 +106,9 @@ struct Tuning {
   // at or above it push; <= 458752, the LDS hub bitmap's bound). 0: from the batch's source
   // count (BitparSolver::pfx_bound)
   int pfx_h = 0;
+  // pull levels probe the any-visited bitmap before a neighbour's row while fewer than this
+  // fraction of the edges lead to visited vertices (ev < filter_frac * nnz)
+  double filter_frac = 0.5;
   int tiles_bpc = 5;
   // code_deg of the tiled level: codes are cheap there (a 4-byte load and LDS ORs instead of a
   // row gather), so rows with up to ~12 expected bits are worth a try (RMAT-26 level 2: 3 ->
@@ -335,7 +338,6 @@ class BitparSolver final : public Solver {
   }
 
   // ---- fixed policy constants (formerly environment knobs; measured, see README)
-  static constexpr double kFilterFrac = 0.5;  // filter unvisited neighbours while ev < frac*nnz
   static constexpr int kWideLater = 1024;     // wide split after the first bottom-up level
   static constexpr int kTdGrid = 1024;        // blocks of the device-driven batches' kernels
   static constexpr int kTdRed = 6;            // fused levels per k_level_reduce_multi launch

@@ -179,7 +179,7 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   const bool tiled = !COUNT && W >= 4 && W >= tun_.tiles_w && tun_.tiles && tun_.pfx == 2 && S.bu_levels == 0 &&
                      S.level == 2 && g_.rows_sorted && n <= INT32_MAX &&
                      n > (int64_t)kHubBig * 32 * 4 &&
-                     ((S.lazy && S.bu_levels == 0) || (double)S.ev < kFilterFrac * (double)g_.nnz) &&
+                     ((S.lazy && S.bu_levels == 0) || (double)S.ev < tun_.filter_frac * (double)g_.nnz) &&
                      pfx_tiles(W, S.part, S.nparts, s) != nullptr;
   S.fl_bitmap = false;  // this level writes its own frontier (list, or bitmap when tiled)
   if (!S.have_active && !tiled) {
@@ -223,9 +223,9 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     snap = asnap_.as<uint32_t>();
   }
   // filtered levels probe the any-visited bitmap before gathering a neighbour's row (while
-  // fewer than kFilterFrac of the edges lead to visited vertices, and always on a lazy batch's
+  // fewer than filter_frac of the edges lead to visited vertices, and always on a lazy batch's
   // first pull); filter_from = first id that is probed (0) or INT32_MAX (no probes)
-  const bool filter = lazy_first || (double)S.ev < kFilterFrac * (double)g_.nnz;
+  const bool filter = lazy_first || (double)S.ev < tun_.filter_frac * (double)g_.nnz;
   const int32_t filter_from = filter ? 0 : INT32_MAX;
   // probes of the lowest ids (the hubs after degree relabelling) read an LDS copy of their
   // bitmap words: 56 KB (ids < 458752, two blocks per CU) or, where one 1024-thread block per CU
@@ -522,7 +522,7 @@ bool BitparSolver::bu_batch_ok(const Loop& S) const {
   if (COUNT || tun_.bu_max <= 0 || tun_.batch <= 1 || !S.have_active || S.bu_levels < 2 ||
       S.old_stale || S.fsrc_acc || S.na > tun_.bu_max || !S.plan.empty() || tun_.dirs.size() > S.level)
     return false;
-  if ((double)S.ev < kFilterFrac * (double)g_.nnz) return false;  // level_bu would filter
+  if ((double)S.ev < tun_.filter_frac * (double)g_.nnz) return false;  // level_bu would filter
   if (tun_.lean && !S.lean_off && S.nact >= tun_.lean_min) return false;
   return S.stop_level == 0xFFFFFFFFu || S.level + 2 <= S.stop_level;
 }

@@ -51,6 +51,7 @@ void Tuning::set(const std::string& key, const std::string& v) {
   else if (key == "dskip3") dskip3 = (int)to_num(key, v);
   else if (key == "chunk2") chunk2 = (int)to_num(key, v);
   else if (key == "wide_few") wide_few = (int)to_num(key, v);
+  else if (key == "filter_frac") filter_frac = to_num(key, v);
   else if (key == "pfx_h") {
     pfx_h = (int)to_num(key, v);
     if (pfx_h < 0 || pfx_h > 458752) fail("tuning: pfx_h must be in [0, 458752]");
@@ -65,7 +66,7 @@ void Tuning::set(const std::string& key, const std::string& v) {
     dirs = v;
   } else {
     fail("tuning: unknown key '" + key +
-         "' (gamma gamma2 pfx codes code_deg lean lean_min lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip push_after dskip3 chunk2 wide_few pfx_h tiles_w dirs)");
+         "' (gamma gamma2 pfx codes code_deg lean lean_min lazy td_fused td_bm batch bu_max tiles tiles_code_deg full dskip push_after dskip3 chunk2 wide_few pfx_h filter_frac tiles_w dirs)");
   }
 }
 

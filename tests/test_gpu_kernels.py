@@ -297,7 +297,9 @@ def test_bitpar_prefix_bound(msbfs_pkg, K):
     qs = m.QuerySet.random(g.n, K, 16, seed=K + 3)
     runs = {"auto": {}, "full": {"pfx_h": 458752}, "h1024": {"pfx_h": 1024},
             "h32768": {"pfx_h": 32768}, "h5000": {"pfx_h": 5000}, "off": {"pfx": 0},
-            "td3": {"dirs": "TBT"}, "td3h1024": {"dirs": "TBT", "pfx_h": 1024}}
+            "td3": {"dirs": "TBT"}, "td3h1024": {"dirs": "TBT", "pfx_h": 1024},
+            # every pull level filtered by the any-visited bitmap / none but the lazy first one
+            "filter_all": {"filter_frac": 2}, "filter_none": {"filter_frac": 0}}
     out = {}
     for name, tun in runs.items():
         with m.Solver(g, "bitpar", max_groups=qs.K, tuning=tun) as s:
