@@ -430,7 +430,16 @@ __global__ __launch_bounds__(BT, MINW) void k_bu_narrow(
       }
     }
     if constexpr (PFX) {  // bits pushed from the tail frontier (k_push_tail)
-      if (valid && stamp[v] == epoch) {
+      if (!stamp) {  // (uniform) no stamps: every vertex reads its row, clears it if set
+        const V<VW> a0 = ldv<VW>(pacc + (int64_t)(valid ? v : 0) * W + slot * VW);
+        bool set = false;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          acc.w[j] = valid ? a0.w[j] : 0ull;
+          set |= acc.w[j] != 0;
+        }
+        if (set) stv<VW>(pacc + (int64_t)v * W + slot * VW, vzero<VW>());
+      } else if (valid && stamp[v] == epoch) {
         acc = ldv<VW>(pacc + (int64_t)v * W + slot * VW);
         stv<VW>(pacc + (int64_t)v * W + slot * VW, vzero<VW>());
       }

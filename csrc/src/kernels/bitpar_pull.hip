@@ -295,12 +295,15 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   }
   // (see k_push_tail_after; needs the whole level in one tiles launch and vertex part 0 of 1)
   S.push_after = pfx && tiled && tun_.push_after && S.nparts == 1 && !S.on_chunk;
+  // no stamps for the per-vertex prefix pull at <= 4 words: it reads every vertex's pushed row
+  // (8W coalesced bytes) instead of a stamp, and the push stores no stamp per edge
+  const bool pfx_nostamp = pfx && !tiled && W <= 4;
   if (pfx && !S.push_after) {
     ++epoch_;
     k_push_tail<W><<<grid_for(S.nf * 64, kBlock, 8192), kBlock, 0, s>>>(
         fl_[S.fc].as<int32_t>(), S.nf, H, g_.rowptr, g_.col, R, codes, code_from,
         tiled ? nullptr : done_.as<uint32_t>(), S.part, S.nparts, acc_[S.ac].as<uint64_t>(),
-        tiled ? nullptr : stamp_.as<int32_t>(), epoch_);
+        (tiled || pfx_nostamp) ? nullptr : stamp_.as<int32_t>(), epoch_);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   if (tiled) {
@@ -336,7 +339,8 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                            ctr_.as<Ctr>(),
                            anyvis_.as<uint32_t>(), filter_from, actw_[1].as<int32_t>(),
                            next_wide, slabF<W>(rows), acc_[S.ac].as<uint64_t>(),
-                           stamp_.as<int32_t>(), epoch_, plen, nullptr, snap, BuGate{});
+                           pfx_nostamp ? nullptr : stamp_.as<int32_t>(), epoch_, plen, nullptr,
+                           snap, BuGate{});
       if (FUSE) rows += gn;
     } else if (hub_lds) {
       constexpr int BT = 1024;
