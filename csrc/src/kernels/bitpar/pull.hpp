@@ -9,13 +9,16 @@ namespace msbfs {
 namespace bp {
 
 // build the bottom-up active lists (deg > 0, not done) over the vertices v = part + i*nparts,
-// i < cnt, split by degree (nparts = 1: every vertex; the hybrid mode's vertex-partitioned
-// level pulls only for its own residue class)
+// i < cnt, split by degree, or by the row prefix length plen[v] when given (the untiled prefix
+// level pulls only the prefix: a vertex of high degree with a short prefix is a narrow one)
+// (nparts = 1: every vertex; the hybrid mode's vertex-partitioned level pulls only for its own
+// residue class)
 template <int QCAP>
 __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, int nparts,
                                                          const int64_t* rowptr,
                                                          const uint32_t* done, int wide_deg,
-                                                         int32_t* act, int32_t* actw, Ctr* ctr) {
+                                                         int32_t* act, int32_t* actw, Ctr* ctr,
+                                                         const int32_t* plen = nullptr) {
   // Each block owns QCAP consecutive list positions j and flushes its narrow queue once at the
   // end (one counter atomic per QCAP vertices: atomics on one address serialise, and 64K of them
   // were most of this kernel's time on 33M vertices). Blocks are dispatched in order, so the
@@ -34,17 +37,19 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
   unsigned long long eu = 0;
   const int64_t b0 = (int64_t)blockIdx.x * QCAP, b1 = min(b0 + (int64_t)QCAP, cnt);
   for (int64_t b = b0; b < b1; b += kStep) {
-    int64_t d[VPT];
+    int64_t d[VPT], sd[VPT];
     uint32_t dw[VPT];
 #pragma unroll
     for (int q = 0; q < VPT; ++q) {
       const int64_t j = b + q * kBlock + threadIdx.x;
       const int64_t i = part + j * nparts;
       d[q] = 0;
+      sd[q] = 0;
       dw[q] = ~0u;
       if (j < b1) {
         d[q] = rowptr[i + 1] - rowptr[i];
         dw[q] = done[i >> 5];
+        sd[q] = plen ? (int64_t)plen[i] : d[q];
       }
     }
 #pragma unroll
@@ -52,8 +57,8 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
       const int64_t i = part + (b + q * kBlock + threadIdx.x) * nparts;
       const bool ok = d[q] > 0 && !((dw[q] >> (i & 31)) & 1u);
       if (ok) eu += (unsigned long long)d[q];
-      q_push(qn, ok && d[q] <= wide_deg, (int32_t)i);
-      q_push(qw, ok && d[q] > wide_deg, (int32_t)i);
+      q_push(qn, ok && sd[q] <= wide_deg, (int32_t)i);
+      q_push(qw, ok && sd[q] > wide_deg, (int32_t)i);
     }
     q_flush(qw, actw, &ctr->actw2.v, (int)kStep, false);
   }
@@ -152,7 +157,8 @@ static __global__ __launch_bounds__(kBlock) void k_count_wide(const int64_t* row
 // visited bitmap for every neighbour id >= H (the degree tail: ~40 % of the edge endpoints on
 // RMAT-26, almost none of them in the level-1 frontier). Instead the pulls stop at the first id
 // >= H, and the few level-1 frontier vertices u >= H push their bits to their neighbours here:
-// acc[v] |= row(u) (atomicOr, mostly one word thanks to the sparse codes) and stamp[v] = epoch.
+// acc[v] |= row(u) (atomicOr, mostly one word thanks to the sparse codes) and stamp[v] = epoch
+// (stamp = nullptr: the consumer reads every vertex's acc row instead).
 // The narrow pull folds acc[v] of stamped vertices into its accumulator (and clears it); wide
 // vertices collect it with their chunk results in k_bu_wide_finalize. Sources need no push:
 // every neighbour of a source was reached at level 1. Only own vertices (v % nparts == part) are
@@ -163,39 +169,70 @@ template <int W>
 __global__ __launch_bounds__(kBlock) void k_push_tail(
     const int32_t* fl, int64_t nf, int32_t H, const int64_t* rowptr, const int32_t* col,
     const uint64_t* R, const uint32_t* code, int32_t code_from, const uint32_t* done,
-    int part, int nparts, uint64_t* acc, int32_t* stamp, int32_t epoch) {
-  // 16 lanes per frontier entry, 4 entries per wave in flight (tail vertices have tens to a few
-  // hundred neighbours; the lanes of an entry take consecutive row entries)
-  constexpr int PG = 64;
+    int part, int nparts, uint64_t* acc, int32_t* stamp, int32_t epoch, int split) {
+  constexpr int PG = 64;  // lanes per wave: an entry's lanes take consecutive row entries
+  // `split` waves per frontier entry (wave s of entry i takes row entries s*64 + lane, step
+  // split*64; the host splits small frontiers only), UN entries per lane in flight: a frontier
+  // vertex of degree 30K otherwise kept one wave busy for ~470 dependent rounds of column id ->
+  // done probe -> atomic while the rest of the grid had finished (RMAT-30 / 32 groups: ~10K
+  // frontier vertices push; 1024 groups: ~100K+, mostly of low degree, one wave each)
+  constexpr int UN = 4;
+  const int SPLIT = split;
   // own targets: v % nparts == part (hybrid phase A); a power-of-two count tests the low bits
   // instead of dividing (v % nparts: ~40 VALU per neighbour entry)
   const uint32_t pmask = (nparts & (nparts - 1)) == 0 ? (uint32_t)(nparts - 1) : 0u;
-  const int lane = lane_id(), slot = lane % PG;
-  const int64_t grp = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / PG;
-  const int64_t ngrp = ((int64_t)gridDim.x * kBlock) / PG;
-  for (int64_t i = grp; i < nf; i += ngrp) {
+  const int lane = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / PG;
+  const int64_t nwave = ((int64_t)gridDim.x * kBlock) / PG;
+  for (int64_t wi = wave; wi < nf * SPLIT; wi += nwave) {
+    const int64_t i = wi / SPLIT;
+    const int sp = (int)(wi % SPLIT);
     const int32_t u = fl[i];
     if (u < H) continue;
     const uint32_t c = (code && u >= code_from) ? code[u] : kDenseCode;
     if (c == 0) continue;
     const int64_t b = rowptr[u], e = rowptr[u + 1];
-    for (int64_t k = b + slot; k < e; k += PG) {
-      const int32_t v = col[k];
-      if (nparts > 1 && (pmask ? ((uint32_t)v & pmask) != (uint32_t)part : v % nparts != part))
-        continue;
-      if (done && is_done(done, v)) continue;  // (nullptr: the consumer clears done rows too)
-      if (c != kDenseCode) {
-        for (int i = 0; i < kCodeSlots; ++i) {
-          const int g = code_g(c, i);
-          if (g >= 0) atomicOr((unsigned long long*)&acc[(int64_t)v * W + (g >> 6)], 1ull << (g & 63));
-        }
-      } else {
-        for (int j = 0; j < W; ++j) {
-          const uint64_t w = R[(int64_t)u * W + j];
-          if (w) atomicOr((unsigned long long*)&acc[(int64_t)v * W + j], (unsigned long long)w);
-        }
+    const int64_t kStep = (int64_t)SPLIT * PG;
+    for (int64_t k0 = b + sp * PG + lane; k0 < e; k0 += UN * kStep) {
+      int32_t v[UN];
+      bool ok[UN];
+#pragma unroll
+      for (int q = 0; q < UN; ++q) {  // loads first (clamped index), tests after
+        const int64_t k = k0 + q * kStep;
+        const int32_t x = col[k < e ? k : k0];
+        v[q] = x;
+        ok[q] = k < e;
       }
-      if (stamp) stamp[v] = epoch;  // (nullptr: the tiled pull reads every acc row instead)
+#pragma unroll
+      for (int q = 0; q < UN; ++q)
+        if (nparts > 1)
+          ok[q] = ok[q] && (pmask ? ((uint32_t)v[q] & pmask) == (uint32_t)part
+                                  : v[q] % nparts == part);
+      if (done) {  // (nullptr: the consumer clears done rows too)
+        uint32_t dw[UN];
+#pragma unroll
+        for (int q = 0; q < UN; ++q) dw[q] = done[v[q] >> 5];
+#pragma unroll
+        for (int q = 0; q < UN; ++q) ok[q] = ok[q] && !((dw[q] >> (v[q] & 31)) & 1u);
+      }
+#pragma unroll
+      for (int q = 0; q < UN; ++q) {
+        if (!ok[q]) continue;
+        if (c != kDenseCode) {
+          for (int s = 0; s < kCodeSlots; ++s) {
+            const int g = code_g(c, s);
+            if (g >= 0)
+              atomicOr((unsigned long long*)&acc[(int64_t)v[q] * W + (g >> 6)], 1ull << (g & 63));
+          }
+        } else {
+          for (int j = 0; j < W; ++j) {
+            const uint64_t w = R[(int64_t)u * W + j];
+            if (w)
+              atomicOr((unsigned long long*)&acc[(int64_t)v[q] * W + j], (unsigned long long)w);
+          }
+        }
+        if (stamp) stamp[v[q]] = epoch;  // (nullptr: the consumer reads every acc row)
+      }
     }
   }
 }

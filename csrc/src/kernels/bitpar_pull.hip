@@ -182,6 +182,20 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                      ((S.lazy && S.bu_levels == 0) || (double)S.ev < tun_.filter_frac * (double)g_.nnz) &&
                      pfx_tiles(W, S.part, S.nparts, s) != nullptr;
   S.fl_bitmap = false;  // this level writes its own frontier (list, or bitmap when tiled)
+  // The untiled prefix level with a low prefix bound (few sources, see pfx_bound) splits its
+  // lists by prefix length (k_build_active): most vertices of degree > wide_few then have short
+  // prefixes, which the per-vertex pull handles in a few steps instead of a hub chunk each.
+  // RMAT-30 / 32 groups (H ~32K): 53.3 -> 51.2 ms per step (level 2 27.0 -> 23.5, levels 3-4
+  // +1.4); RMAT-26 / 16 groups (H ~84K) 4.99 -> 4.92; with H >= ~300K (64+ groups on RMAT-26)
+  // 0.4-0.6 ms slower, so only below H = 131072. (The predicate is `pfx` below, evaluated
+  // before the level's state moves on.)
+  constexpr int32_t kHubN = kHubW * 32;
+  const bool pfx_lists = !tiled && tun_.pfx == 2 && S.bu_levels == 0 && S.level == 2 &&
+                         pfx_bound<W>(S) <= 131072 &&
+                         ((S.lazy && S.bu_levels == 0) ||
+                          (double)S.ev < tun_.filter_frac * (double)g_.nnz) &&
+                         n > (int64_t)kHubN * 4 && n > (int64_t)kHubBig * 32 * 4 &&
+                         g_.rows_sorted && n <= INT32_MAX;
   if (!S.have_active && !tiled) {
     // after the first bottom-up level most vertices exit early: a whole wave per chunk pays
     // off only for much higher degrees, so later lists are split at a higher threshold
@@ -194,7 +208,8 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
                           : opt.wide_degree;
     k_build_active<4096><<<grid_for(S.cnt, 4096, INT32_MAX), kBlock, 0, s>>>(
         S.cnt, S.part, S.nparts, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
-        actw_[0].as<int32_t>(), ctr_.as<Ctr>());
+        actw_[0].as<int32_t>(), ctr_.as<Ctr>(),
+        pfx_lists ? prefix_lens(pfx_bound<W>(S), s) : nullptr);
     MSBFS_HIP_CHECK(hipGetLastError());
     const HostCtr c = read_ctr(s);
     S.nact = c.act2;
@@ -300,10 +315,11 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
   const bool pfx_nostamp = pfx && !tiled && W <= 4;
   if (pfx && !S.push_after) {
     ++epoch_;
-    k_push_tail<W><<<grid_for(S.nf * 64, kBlock, 8192), kBlock, 0, s>>>(
+    const int split = S.nf < 65536 ? 8 : 1;  // (see k_push_tail)
+    k_push_tail<W><<<grid_for(S.nf * 64 * split, kBlock, 8192), kBlock, 0, s>>>(
         fl_[S.fc].as<int32_t>(), S.nf, H, g_.rowptr, g_.col, R, codes, code_from,
         tiled ? nullptr : done_.as<uint32_t>(), S.part, S.nparts, acc_[S.ac].as<uint64_t>(),
-        (tiled || pfx_nostamp) ? nullptr : stamp_.as<int32_t>(), epoch_);
+        (tiled || pfx_nostamp) ? nullptr : stamp_.as<int32_t>(), epoch_, split);
     MSBFS_HIP_CHECK(hipGetLastError());
   }
   if (tiled) {
