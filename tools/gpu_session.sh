@@ -39,6 +39,8 @@ for s in "$@"; do
     trace128) MSBFS_TRACE=1 step trace128 300 python bench.py --steps 2 --warmup 1 --groups 128 ;;
     prof26) prof prof26 600 python bench.py --steps 1 --warmup 0 --verify 0 ;;
     prof128) prof prof128 600 python bench.py --groups 128 --steps 1 --warmup 0 --verify 0 ;;
+    prof256) prof prof256 600 python bench.py --groups 256 --steps 1 --warmup 0 --verify 0 ;;
+    prof512) prof prof512 600 python bench.py --groups 512 --steps 1 --warmup 0 --verify 0 ;;
     prof30) prof prof30 900 python bench.py --scale 30 --groups 32 --steps 1 --warmup 1 --verify 0 ;;
     prof22) prof prof22 300 python bench.py --scale 22 --groups 64 --steps 3 --warmup 1 --verify 0 ;;
     rmat22) step rmat22 300 python bench.py --scale 22 --groups 64 --steps 5 --warmup 1 --verify 16 ;;
