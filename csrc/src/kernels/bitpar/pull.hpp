@@ -18,7 +18,11 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
                                                          const int64_t* rowptr,
                                                          const uint32_t* done, int wide_deg,
                                                          int32_t* act, int32_t* actw, Ctr* ctr,
-                                                         const int32_t* plen = nullptr) {
+                                                         const int32_t* plen = nullptr,
+                                                         int64_t n_eff = -1) {
+  // n_eff >= 0 (with plen, degree-relabelled rows: exactly the vertices < n_eff have edges): no
+  // row offsets are read at all (RMAT-30: 8.6 GB), and eu2 stays 0 (its caller reads only the
+  // list sizes)
   // Each block owns QCAP consecutive list positions j and flushes its narrow queue once at the
   // end (one counter atomic per QCAP vertices: atomics on one address serialise, and 64K of them
   // were most of this kernel's time on 33M vertices). Blocks are dispatched in order, so the
@@ -47,16 +51,21 @@ __global__ __launch_bounds__(kBlock) void k_build_active(int64_t cnt, int part, 
       sd[q] = 0;
       dw[q] = ~0u;
       if (j < b1) {
-        d[q] = rowptr[i + 1] - rowptr[i];
+        if (n_eff >= 0) {
+          d[q] = i < n_eff ? 1 : 0;
+          if (i < n_eff) sd[q] = (int64_t)plen[i];
+        } else {
+          d[q] = rowptr[i + 1] - rowptr[i];
+          sd[q] = plen ? (int64_t)plen[i] : d[q];
+        }
         dw[q] = done[i >> 5];
-        sd[q] = plen ? (int64_t)plen[i] : d[q];
       }
     }
 #pragma unroll
     for (int q = 0; q < VPT; ++q) {
       const int64_t i = part + (b + q * kBlock + threadIdx.x) * nparts;
       const bool ok = d[q] > 0 && !((dw[q] >> (i & 31)) & 1u);
-      if (ok) eu += (unsigned long long)d[q];
+      if (ok && n_eff < 0) eu += (unsigned long long)d[q];
       q_push(qn, ok && sd[q] <= wide_deg, (int32_t)i);
       q_push(qw, ok && sd[q] > wide_deg, (int32_t)i);
     }

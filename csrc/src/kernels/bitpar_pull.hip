@@ -209,7 +209,8 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     k_build_active<4096><<<grid_for(S.cnt, 4096, INT32_MAX), kBlock, 0, s>>>(
         S.cnt, S.part, S.nparts, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
         actw_[0].as<int32_t>(), ctr_.as<Ctr>(),
-        pfx_lists ? prefix_lens(pfx_bound<W>(S), s) : nullptr);
+        pfx_lists ? prefix_lens(pfx_bound<W>(S), s) : nullptr,
+        (pfx_lists && g_.old2new) ? n_eff() : -1);  // (degree-relabelled: no isolated id < n_eff)
     MSBFS_HIP_CHECK(hipGetLastError());
     const HostCtr c = read_ctr(s);
     S.nact = c.act2;
