@@ -356,7 +356,8 @@ __global__ __launch_bounds__(kBlock) void k_push_tail_after(
 // this block's row of the counter slab, slabF = first row of this launch) instead of by a
 // separate k_count_frontier pass that re-reads both rows of every new frontier vertex.
 // PFX (prefix-pull level, see k_push_tail): rows are scanned only up to the first id >= HUBW*32,
-// and pushed bits (acc of vertices with stamp == epoch) seed the accumulator.
+// and pushed bits (acc of vertices with stamp == epoch; every vertex's acc when stamp is
+// nullptr) seed the accumulator.
 // CS = neighbours per step (rows gathered between two coverage checks).
 // C1 > 0 (unfiltered levels only): a first step of just C1 rows before the CS-wide steps; late
 // levels are mostly covered by the first neighbour or two (sorted rows: hubs first).
