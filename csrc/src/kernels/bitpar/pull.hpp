@@ -355,7 +355,8 @@ __global__ __launch_bounds__(kBlock) void k_push_tail_after(
 // FUSE: the level's new-bit counts are accumulated here (register bit-sliced counters -> LDS ->
 // this block's row of the counter slab, slabF = first row of this launch) instead of by a
 // separate k_count_frontier pass that re-reads both rows of every new frontier vertex.
-// PFX (prefix-pull level, see k_push_tail): rows are scanned only up to the first id >= HUBW*32,
+// PFX (prefix-pull level, see k_push_tail): rows are scanned only over their prefix plen[v] (the
+// ids below the level's bound H <= HUBW*32, see BitparSolver::pfx_bound),
 // and pushed bits (acc of vertices with stamp == epoch; every vertex's acc when stamp is
 // nullptr) seed the accumulator.
 // CS = neighbours per step (rows gathered between two coverage checks).
