@@ -201,11 +201,15 @@ int BitparSolver::level_bu(Loop& S, hipStream_t s) {
     // off only for much higher degrees, so later lists are split at a higher threshold
     // (wide_few only on big graphs: RMAT-22 / 64 groups ran level 2 in 0.66 ms at 32 or 64 and
     // 0.76-0.83 ms at 128; the narrow pull's long rows then have too few vertices to hide behind)
+    // (lists split by prefix length on a graph of >= 2^28 non-isolated vertices: half of it;
+    // RMAT-30 / 32 groups 51.1 -> 49.5 ms at 64, 49.8 at 48, 52.6 at 32 prefix entries, while
+    // RMAT-26 / 16 groups keeps 128: 4.70 ms, 4.84 at 96, 4.95 at 64)
+    const bool few = W <= 4 && tun_.wide_few > 0 && opt.wide_degree == kDefaultWideDegree &&
+                     n_eff() >= ((int64_t)1 << 23);
     const int wide0 = S.bu_levels != 0 ? next_wide
-                      : (W <= 4 && tun_.wide_few > 0 && opt.wide_degree == kDefaultWideDegree &&
-                         n_eff() >= ((int64_t)1 << 23))
-                          ? tun_.wide_few
-                          : opt.wide_degree;
+                      : !few ? opt.wide_degree
+                      : (pfx_lists && n_eff() >= ((int64_t)1 << 28)) ? std::max(1, tun_.wide_few / 2)
+                                                                      : tun_.wide_few;
     k_build_active<4096><<<grid_for(S.cnt, 4096, INT32_MAX), kBlock, 0, s>>>(
         S.cnt, S.part, S.nparts, g_.rowptr, done_.as<uint32_t>(), wide0, act_[0].as<int32_t>(),
         actw_[0].as<int32_t>(), ctr_.as<Ctr>(),
