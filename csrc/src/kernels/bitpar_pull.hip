@@ -84,7 +84,12 @@ int32_t BitparSolver::pfx_bound(const Loop& S) {
   constexpr int32_t kPfxH = 14336 * 32;  // (the LDS hub bitmap's bound, see level_bu)
   if (tun_.pfx_h > 0) return std::min(tun_.pfx_h, kPfxH);
   if (S.nsrc <= 0) return kPfxH;
-  const double md = (double)g_.n / (64.0 * W * (double)S.nsrc);  // degree where the pull pays
+  // (>= 2^28 vertices: 1 / 32 whatever the words, the pull's column stream and the push's
+  // atomics both miss the caches there; RMAT-30 / 128-group passes: H 458752 -> the ~174K
+  // vertices of degree >= 2^14, 209.0 -> 203.8 ms per 256-group step; 32 groups unchanged)
+  const double md = n_eff() >= ((int64_t)1 << 28)
+                        ? (double)g_.n / (32.0 * (double)S.nsrc)
+                        : (double)g_.n / (64.0 * W * (double)S.nsrc);  // degree where the pull pays
   if (md < 2.0) return kPfxH;
   int k = 0;
   while (k + 1 < kDegBounds && (double)((int64_t)1 << (k + 1)) <= md) ++k;  // 2^k <= md
